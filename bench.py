@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""bench.py — the driver's benchmark of mpi_perf's hot path on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]          (N = 1)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A "step" is one run of the reference's loop (mpi_perf.c:474-569: barrier ->
+`iters` x transfer -> barrier) over one batch of synthetic bytes:
+
+* N = 1 — BASELINE config 2, the 1-GPU local device-to-device copy: each step
+  is `iters` launches of the HBM copy kernel moving B = 1 GiB tx -> rx (the
+  loop's degenerate pair, both ends on one GPU).  value = B*iters*K / T.
+* N >= 2 — BASELINE config 4, all-pairs concurrent rounds (run-hbv3-style,
+  unidirectional): step s runs round s mod (N-1) of the circle-method
+  schedule; each of the N/2 pairs moves `iters` x 4 MiB G1 -> G0 over xGMI
+  with the 1-byte ack (mpi_perf.c:127-145).  value = sum of bytes over all
+  pairs / T, with T the max over ranks (weak scaling: every GPU is in one
+  pair per step).
+
+Rank 0 prints one JSON line.  `roofline` is computed for the dominant kernel
+from HIP-event time measured inside this process (libmpx records the events
+on the stream it launches on); `cpu_baseline` times the compiled reference
+(oracle/_ref, under MPICH shared memory) or, if absent, the oracle's CPU port.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import shutil
+import statistics
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
+
+HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+XGMI_LINK_PEAK_GBPS = 153.6  # BASELINE.json north_star: ~153 GB/s per xGMI link
+
+
+def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:
+    """Time the reference on the host: 2 ranks, unidirectional, B bytes."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    sample = f"-u 1 -b {nbytes} -i {iters} -r {runs}, 2 ranks, runs 1..{runs - 1} (run 0 is the reference's warm-up)"
+    if os.path.exists(ref) and os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libshim.so")) \
+            and os.path.exists(mpiexec):
+        tmp = tempfile.mkdtemp(prefix="cpu_base_")
+        try:
+            with open(os.path.join(tmp, "group1"), "w") as f:
+                f.write("localhost\n")
+            os.mkdir(os.path.join(tmp, "logs"))
+            env = dict(os.environ, PPN="1", HOST1="localhost", HOST0="127.0.0.1")
+            env.pop("SHIM_OUT", None)
+            cmd = [mpiexec, "-np", "2", "-genv", "PPN", "1", "-genv", "HOST1", "localhost", "-genv", "HOST0",
+                   "127.0.0.1", os.path.join(ROOT, "oracle", "ref_wrap.sh"), ref, "-f", "group1", "-n", "1",
+                   "-p", "1", "-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs), "-l", "logs"]
+            p = subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=300)
+            times = []
+            for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log")):
+                for line in open(path):
+                    times.append(float(line.split(",")[9]) / 1000.0)
+            if p.returncode == 0 and times:
+                t = statistics.median(times)
+                return dict(value=round(nbytes * iters / t / 1e9, 3), unit="GB/s", cores=2, kind="reference",
+                            sample="mpi_perf.c (oracle/_ref) under MPICH 3.3.2 shm, " + sample,
+                            median_run_s=t)
+            print(f"[bench] reference baseline failed rc={p.returncode}: {p.stderr[-400:]}", file=sys.stderr)
+        except Exception as e:  # noqa: BLE001
+            print(f"[bench] reference baseline unavailable: {e}", file=sys.stderr)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+    port = os.path.join(ROOT, "oracle", "oracle_perf")
+    if os.path.exists(port):
+        p = subprocess.run([port, "-p", "1", "-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs)],
+                           capture_output=True, text=True, timeout=300, env=dict(os.environ, ORACLE_NO_DIGEST="1"))
+        rows = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][1:]
+        if rows:
+            t = statistics.median(r["max_time_s"] for r in rows)
+            return dict(value=round(nbytes * iters / t / 1e9, 3), unit="GB/s", cores=2, kind="port",
+                        sample="oracle/oracle_perf (C restatement, 2 threads), " + sample, median_run_s=t)
+    return None
+
+
+def traffic_from_profile(workload: str) -> dict | None:
+    """Per-launch HBM bytes from the committed PMC summary of this workload
+    (profiles/pmc_<workload>.json, written by tools/pmc_summary.py from
+    rocprofv3 --pmc passes, corrected per MI355X_MICROARCH.md §HBM)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: int = 3) -> dict:
+    """Two ranks on GPU 0 (one host thread each): per-pair time of the loop."""
+    with mpx.Context(2, engine) as c:
+        bufs = []
+        for r in range(2):
+            tx, rx = c.alloc(0, max(nbytes, 1)), c.alloc(0, max(nbytes, 1))
+            c.fill(tx, nbytes, mpx.FILL_BYTE, ord("b") if r == 0 else ord("a"))
+            c.attach(r, 0, tx, rx, nbytes)
+            bufs.append((tx, rx))
+        res = []
+        for _ in range(runs + 1):
+            out = {}
+
+            def side(r):
+                out[r] = c.xfer(mode, 1 - r, r, 1 - r, iters, bufs[r][0], bufs[r][1], nbytes)
+
+            th = [threading.Thread(target=side, args=(r,)) for r in range(2)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            res.append(max(out[0].wall_s, out[1].wall_s))
+        return dict(median_s=statistics.median(res[1:]), per_iter_us=statistics.median(res[1:]) / iters * 1e6)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--engine", default="kernel", choices=["kernel", "sdma", "rccl"])
+    ap.add_argument("--bytes", type=int, default=0, help="message bytes (default: 1 GiB at N=1, 4 MiB at N>1)")
+    ap.add_argument("--iters", type=int, default=0, help="transfers per step (default 10 at N=1, 100 at N>1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+
+    one = world == 1
+    nbytes = args.bytes or ((1 << 30) if one else (4 << 20))
+    iters = args.iters or (10 if one else 100)
+
+    # CPU baseline first, before this process touches the GPU
+    cpu = None
+    if one and rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(nbytes, 16, 4)
+
+    import torch
+    import mpx
+
+    torch.cuda.set_device(local)
+    dist = None
+    if not one:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    extras = {}
+    if one:
+        workload = "local_d2d_copy"
+        c = mpx.Context(1, args.engine)
+        src, dst = c.alloc(0, nbytes), c.alloc(0, nbytes)
+        key = mpx.pattern_key(mpx.PATTERN_SEED, 0, 0, 0)
+        c.fill(src, nbytes, mpx.FILL_SPLITMIX, key)
+        for _ in range(args.warmup):
+            c.copy(0, dst, src, nbytes, iters)
+        dev_s, launches = 0.0, 0
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            t = c.copy(0, dst, src, nbytes, iters)
+            dev_s += t.device_s
+            launches += t.launches
+        barrier_sync()
+        elapsed = time.perf_counter() - t0
+        assert c.checksum(dst, nbytes) == c.checksum(src, nbytes), "copy output differs from its input"
+        total = nbytes * iters * args.steps
+        per_launch = dev_s / max(launches, 1)
+        algo = 2 * nbytes   # read B + write B per launch
+        achieved = algo / per_launch / 1e9
+        roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None, kernel="k_copy<4>",
+                    avg_launch_us=round(per_launch * 1e6, 2), algorithmic_bytes_per_launch=algo)
+        prof = traffic_from_profile(workload)
+        if prof and prof.get("bytes") == nbytes:
+            roof["traffic"] = prof.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = prof.get("source")
+        config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine="kernel (k_copy)",
+                      parallelism="single GPU")
+        metric_unit = "GB/s"
+        if not args.no_extras:
+            lat = loopback_pair(mpx, "kernel", mpx.MODE_PINGPONG, 8, 5000)
+            extras["loopback_pingpong_8B_half_rtt_us"] = round(lat["per_iter_us"] / 2, 3)
+            uni = loopback_pair(mpx, "kernel", mpx.MODE_UNIDIR, 4 << 20, 200)
+            extras["loopback_unidir_4MiB_GBps"] = round((4 << 20) / (uni["per_iter_us"] * 1e-6) / 1e9, 2)
+        c.close()
+    else:
+        from mpx.schedule import all_pairs_rounds, round_role
+        workload = "all_pairs_rounds_unidir"
+        c = mpx.Context(world, args.engine)
+        tx, rx = c.alloc(local, nbytes), c.alloc(local, nbytes)
+        c.fill(tx, nbytes, mpx.FILL_BYTE, ord("b"))
+        c.attach(rank, local, tx, rx, nbytes)
+        descs = [None] * world
+        dist.all_gather_object(descs, c.export(rank))
+        for r in range(world):
+            if r != rank:
+                c.import_rank(r, descs[r])
+        if args.engine == "rccl":
+            uid = [mpx.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            c.rccl_init_rank(rank, world, uid[0])
+        rounds = all_pairs_rounds(world)
+
+        def step(s: int):
+            g, peer = round_role(rounds, s % len(rounds), rank)
+            dist.barrier()                           # MPI_Barrier, mpi_perf.c:499
+            return c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes)
+
+        for s in range(args.warmup):
+            step(s)
+        dev_s, n_sends = 0.0, 0
+        barrier_sync()
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            t = step(s)
+            if round_role(rounds, s % len(rounds), rank)[0] == 1:
+                dev_s += t.device_s
+                n_sends += 1
+        barrier_sync()
+        elapsed = time.perf_counter() - t0
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+        total = (world // 2) * nbytes * iters * args.steps
+        st = torch.tensor([dev_s, float(n_sends)], dtype=torch.float64)
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)
+        per_launch = float(st[0]) / max(float(st[1]), 1.0)
+        algo = nbytes * iters   # bytes one k_xfer launch pushes over its link
+        achieved = algo / per_launch / 1e9
+        roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",
+                    frac=round(achieved / XGMI_LINK_PEAK_GBPS, 4), traffic=None, kernel="k_xfer (G1 side)",
+                    avg_launch_us=round(per_launch * 1e6, 2), algorithmic_bytes_per_launch=algo)
+        config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=args.engine,
+                      rounds=len(rounds), pairs_per_round=world // 2, parallelism=f"pairs{world // 2}")
+        metric_unit = "GB/s"
+        if not args.no_extras:
+            g, peer = round_role(rounds, 0, rank)
+            dist.barrier()
+            lt = c.xfer(mpx.MODE_PINGPONG, g, rank, peer, 2000, tx, rx, 8)
+            lat = torch.tensor([lt.wall_s], dtype=torch.float64)
+            dist.all_reduce(lat, op=dist.ReduceOp.MAX)
+            extras["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / 4000 * 1e6, 3)
+            extras["per_pair_unidir_GBps"] = round(achieved, 2)
+        c.close()
+
+    value = total / elapsed / 1e9
+    if rank == 0:
+        line = {
+            "metric": "per-pair xGMI GB/s at 4 MB + 8 B latency us; all-pairs aggregate GB/s at 2/4/8 GPUs",
+            "value": round(value, 3),
+            "unit": metric_unit,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": config,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "extras": extras,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,196 @@
+/*
+ * mpx.h — C-ABI of libmpx, the MI355X transfer engine behind mpx_perf.
+ *
+ * This is the drop-in boundary for mpi_perf's hot path.  In the reference the
+ * seam is the transfer-loop signature shared by the three loops
+ *
+ *   void do_mpi_benchmark*(int my_group, int my_rank, int peer_rank,
+ *                          char *peer_host, char *my_host, int iters,
+ *                          void *buffer_tx, void *buffer_rx, int buff_len)
+ *
+ *   (/root/reference/mpi_perf.c:66-67, :85-86, :127-128), called from main
+ *   between t_start and t_end_local (mpi_perf.c:501-532) on buffers made by
+ *   allocate_tx_rx_buffers (mpi_perf.c:240-252) and freed by main (:574-578).
+ *
+ * mpx_xfer() keeps that argument order (minus the two host strings, plus the
+ * loop mode and an out-parameter for the elapsed time).  Every other entry
+ * point replaces one MPI/libc call the reference makes around the loop; each
+ * declaration cites the call it replaces.
+ *
+ * Conventions
+ *  - Every function returns an int status: MPX_OK (0) or an MPX_ERR_* code;
+ *    mpx_strerror() turns it into text.  The host wraps calls in MPX_CHECK,
+ *    which mirrors the reference's MPI_CHECK print-and-exit (mpi_perf.c:55-64).
+ *  - Plain pointers and sizes only; no HIP, RCCL or torch types cross the ABI.
+ *  - Ownership: the caller allocates (mpx_alloc) and frees (mpx_free) tx/rx;
+ *    transfer calls borrow them, exactly like the reference's loops.
+ *  - Threading: one context may be shared by several host threads, one per
+ *    rank; calls for different ranks may run concurrently.  Calls for the same
+ *    rank must not.
+ *  - A "rank" is a logical endpoint (the reference's MPI rank).  A rank lives
+ *    on one GPU.  Ranks of the same context are "local" (attached with
+ *    mpx_rank_attach); ranks living in another process are "imported" from
+ *    the descriptor that process exported (mpx_rank_export/mpx_rank_import).
+ */
+#ifndef MPX_H
+#define MPX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPX_ABI_VERSION 1
+#define MPX_MAX_RANKS 16          /* ranks one context can address           */
+#define MPX_RANK_DESC_BYTES 512   /* size of the opaque exported descriptor  */
+#define MPX_RCCL_ID_BYTES 128     /* size of an RCCL unique id               */
+
+/* ---- status codes ------------------------------------------------------ */
+enum mpx_status {
+    MPX_OK = 0,
+    MPX_ERR_INVALID = 1,      /* bad argument (null, range, unknown rank)   */
+    MPX_ERR_HIP = 2,          /* a HIP runtime call failed                  */
+    MPX_ERR_NOMEM = 3,        /* device allocation failed                   */
+    MPX_ERR_TIMEOUT = 4,      /* a device-side wait exceeded its deadline   */
+    MPX_ERR_RCCL = 5,         /* an RCCL call failed                        */
+    MPX_ERR_UNSUPPORTED = 6,  /* engine/mode combination not available      */
+    MPX_ERR_STATE = 7,        /* call out of order (not attached, no comm)  */
+    MPX_ERR_CHECK = 8         /* a received payload failed its checksum     */
+};
+
+/* ---- transfer engines (north_star (a)/(b)/(c)) ------------------------- */
+enum mpx_engine {
+    MPX_ENGINE_KERNEL = 0,    /* hand-written CDNA4 push kernels + device flags */
+    MPX_ENGINE_SDMA = 1,      /* hipMemcpyPeerAsync + stream wait/write value   */
+    MPX_ENGINE_RCCL = 2       /* ncclSend/ncclRecv                              */
+};
+
+/* ---- loop modes: the three reference loops ----------------------------- */
+enum mpx_mode {
+    MPX_MODE_PINGPONG = 0,    /* do_mpi_benchmark             mpi_perf.c:66-83   */
+    MPX_MODE_NONBLOCKING = 1, /* do_mpi_benchmark_nonblocking mpi_perf.c:85-125  */
+    MPX_MODE_UNIDIR = 2       /* do_mpi_benchmark_unidir      mpi_perf.c:127-145 */
+};
+
+/* ---- fill patterns ----------------------------------------------------- */
+enum mpx_fill {
+    MPX_FILL_BYTE = 0,        /* memset(ptr, arg & 0xff, n): the reference's
+                                 'a'/'b' tx fill, mpi_perf.c:244-251           */
+    MPX_FILL_SPLITMIX = 1     /* 64-bit word k = splitmix64(arg ^ k), tail
+                                 bytes little-endian from the same word        */
+};
+
+/* key for MPX_FILL_SPLITMIX: seed ^ src<<56 ^ dst<<48 ^ iter<<24 */
+#define MPX_PATTERN_SEED 0x6d70695f70657266ULL
+static inline uint64_t mpx_pattern_key(uint64_t seed, unsigned src, unsigned dst,
+                                       unsigned iter)
+{
+    return seed ^ ((uint64_t)src << 56) ^ ((uint64_t)dst << 48) ^ ((uint64_t)iter << 24);
+}
+
+/* ---- timing / statistics of one transfer call ---------------------------- */
+typedef struct mpx_timing {
+    double wall_s;            /* host wall clock around the loop (MPI_Wtime
+                                 analogue, mpi_perf.c:501,532-533)             */
+    double device_s;          /* hipEvent time of the loop on the rank's stream */
+    uint64_t bytes;           /* algorithmic bytes of the loop (a9 formula:
+                                 B*iters*(unidir?1:2), mpi_perf.c:538)         */
+    int32_t launches;         /* kernels / copies issued for the loop          */
+    int32_t nwg;              /* workgroups of the data push (kernel engine)   */
+    int32_t protocol;         /* 0 = LL granules, 1 = bulk+flags, 2 = SDMA,
+                                 3 = RCCL, 4 = local copy kernel               */
+    int32_t check_failures;   /* iterations whose payload checksum mismatched  */
+    uint64_t check_iters;     /* iterations whose payload was checksummed      */
+} mpx_timing;
+
+/* options of mpx_xfer_ex beyond the reference seam */
+typedef struct mpx_xfer_opts {
+    int32_t check;            /* 1: checksum + poison every received payload   */
+    int32_t reserved0;
+    uint64_t expect_checksum; /* mpx_checksum() of the peer's tx[0:len) (B-byte
+                                 receives) — required when check = 1           */
+    uint64_t expect_ack;      /* mpx_checksum() of the peer's tx[0:1) (unidir
+                                 G1's 1-byte acks)                             */
+    uint32_t timeout_ms;      /* per-wait device deadline; 0 = default (10 s)  */
+    int32_t nwg;              /* override push workgroups; 0 = automatic        */
+} mpx_xfer_opts;
+
+/* opaque context */
+typedef struct mpx_ctx mpx_ctx;
+
+/* ---- library ------------------------------------------------------------ */
+int mpx_version(void);
+const char *mpx_strerror(int status);
+/* detail of the last failing call on this thread ("" if none) */
+const char *mpx_last_error(void);
+/* number of visible GPUs (replaces MPI_Comm_size's role of sizing the job,
+   mpi_perf.c:375, for the one-process/many-GPU launch) */
+int mpx_device_count(int *count);
+
+/* MPI_Init analogue (mpi_perf.c:372): a context able to address `nranks`
+   ranks (<= MPX_MAX_RANKS) with the given engine. */
+int mpx_init(int nranks, int engine, mpx_ctx **ctx);
+/* MPI_Finalize analogue (mpi_perf.c:581) */
+int mpx_finalize(mpx_ctx *ctx);
+
+/* ---- buffers (allocate_tx_rx_buffers, mpi_perf.c:240-252) ---------------- */
+/* posix_memalign(4096) analogue: device memory on `dev`, 4 KiB aligned.  The
+   allocation is exportable to other processes (IPC) and peer-mappable. */
+int mpx_alloc(mpx_ctx *ctx, int dev, size_t bytes, void **ptr);
+/* free() analogue (mpi_perf.c:576-577) */
+int mpx_free(mpx_ctx *ctx, void *ptr);
+/* memset analogue (mpi_perf.c:246,250); see enum mpx_fill */
+int mpx_fill(mpx_ctx *ctx, int dev, void *ptr, size_t n, int pattern, uint64_t arg);
+/* order-independent 64-bit checksum of n bytes (definition in DESIGN.md and
+   oracle/mpx_oracle.c: oracle_checksum) */
+int mpx_checksum(mpx_ctx *ctx, int dev, const void *ptr, size_t n, uint64_t *out);
+/* device -> host copy, for tests */
+int mpx_read(mpx_ctx *ctx, int dev, void *host_dst, const void *dev_src, size_t n);
+
+/* ---- local device-to-device copy (BASELINE config 2) --------------------- */
+/* `iters` back-to-back launches of the HBM copy kernel dst[0:n) = src[0:n) on
+   `dev`; the 1-GPU degenerate case of the loop (tx -> rx, no peer). */
+int mpx_copy(mpx_ctx *ctx, int dev, void *dst, const void *src, size_t n, int iters,
+             mpx_timing *t);
+
+/* ---- ranks: pairing/registration (get_peer_rank, mpi_perf.c:200-238) ----- */
+/* Register a rank of this process: its GPU, tx/rx (from mpx_alloc on `dev`)
+   and the largest message it will move.  Allocates the rank's mailbox (flag
+   words + LL landing zone) and stream. */
+int mpx_rank_attach(mpx_ctx *ctx, int rank, int dev, void *tx, void *rx, size_t len);
+/* Serialise a local rank into MPX_RANK_DESC_BYTES bytes for another process
+   (replaces the node_info Allgather, mpi_perf.c:223-224). */
+int mpx_rank_export(mpx_ctx *ctx, int rank, void *desc);
+/* Map a rank exported by another process (IPC) into this context. */
+int mpx_rank_import(mpx_ctx *ctx, int rank, const void *desc);
+
+/* ---- the hot loop -------------------------------------------------------- */
+/* do_mpi_benchmark* replacement.  Runs `iters` iterations of `mode` between
+   local rank `my_rank` (group `my_group`, 1 = sender side) and `peer_rank`,
+   returning when this rank's side of the loop is complete, like the MPI loop.
+   tx/rx must be the buffers attached for my_rank; buff_len <= attached len.
+   *sec (may be NULL) receives the wall time of the loop. */
+int mpx_xfer(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
+             void *tx, void *rx, int buff_len, double *sec);
+/* same, with options (checksum mode, timeouts) and full timing */
+int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
+                void *tx, void *rx, int buff_len, const mpx_xfer_opts *opts, mpx_timing *t);
+
+/* MPI_Barrier analogue (mpi_perf.c:499,557,579) for the threads of ONE
+   process: blocks until `nthreads` callers have entered with the same ctx.
+   Multi-process hosts use their own barrier. */
+int mpx_barrier(mpx_ctx *ctx, int nthreads);
+
+/* ---- RCCL engine setup ---------------------------------------------------- */
+int mpx_rccl_get_unique_id(void *id /* MPX_RCCL_ID_BYTES */);
+/* one rank per process (multi-process hosts) */
+int mpx_rccl_init_rank(mpx_ctx *ctx, int rank, int nranks, const void *id);
+/* every attached local rank of this process, in one call (threads host) */
+int mpx_rccl_init_all(mpx_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPX_H */

@@ -1,0 +1,94 @@
+// mpx_internal.h — types shared by the libmpx runtime (mpx_runtime.hip) and
+// its device code (mpx_kernels.hip).  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/mpx.h"
+
+typedef unsigned long long u64;
+
+namespace mpx {
+
+constexpr int kBlock = 256;              // threads per workgroup = 4 wave64
+constexpr int kMaxPushWG = 256;          // flag slots per (receiver, sender) link
+constexpr int kLLMaxBytes = 8192;        // messages <= this go as LL granules
+constexpr int kLLGranules = kLLMaxBytes / 4;   // 4 payload bytes per granule
+constexpr int kNbWindow = 256;           // MAX_REQ_NUM, mpi_perf.c:88
+
+// Protocol ids reported in mpx_timing.protocol
+enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4 };
+
+// One rank's receive mailbox, in that rank's HBM (uncached / fine-grained so a
+// poll sees stores that arrive over xGMI).  Written ONLY by senders, polled
+// only by the owner.
+//   flag[s][w] : sequence number of the last bulk push workgroup w of sender
+//                rank s finished into this rank's rx (written with one
+//                system-scope store after that workgroup's payload drained)
+//   ll[s][g]   : LL granule g of the current small message from sender s:
+//                {tag:32 | payload:32}, tag = ll_tag(seq), one 8-byte store
+struct Mailbox {
+    u64 flag[MPX_MAX_RANKS][kMaxPushWG];
+    u64 ll[MPX_MAX_RANKS][kLLGranules];
+};
+
+// Per-rank host-mapped status words (written by the device, read by the host
+// after the stream drains).
+struct Status {
+    unsigned int err;       // bit0: a wait timed out
+    unsigned int where;     // 1 + iteration index of the first timeout
+    u64 spins;              // diagnostics: polls of the last wait
+};
+
+// Arguments of one transfer loop on one rank (kernel engine).
+struct XferArgs {
+    const unsigned char* tx;     // local tx
+    unsigned char* rx;           // local rx
+    unsigned char* peer_rx;      // the peer's rx, mapped into this process
+    Mailbox* my_mb;              // local mailbox (polled)
+    Mailbox* peer_mb;            // peer's mailbox (written)
+    Status* status;              // host-mapped
+    u64* csum;                   // [iters] raw checksum sums (check mode)
+    u64* gbar;                   // grid-barrier counter (check mode), zeroed
+    u64 tx_seq0;                 // my last push seq on this link before the call
+    u64 rx_seq0;                 // peer's last push seq on this link
+    u64 timeout_ticks;           // s_memrealtime ticks (100 MHz) per wait
+    long long len;               // B
+    int iters;
+    int mode;                    // enum mpx_mode
+    int group;                   // 1 = sender side (group 1), 0 = group 0
+    int my_slot;                 // my rank = my slot in the peer's mailbox
+    int peer_slot;               // peer rank = its slot in my mailbox
+    int nwg;                     // bulk push workgroups (same on both sides)
+    int check;                   // 1 = checksum + poison each received payload
+};
+
+// LL granule tag for push sequence number `seq` (>= 1): never 0, so a zeroed
+// mailbox can never match, and distinct for seqs < 2^31 apart.
+__host__ __device__ inline unsigned ll_tag(u64 seq) {
+    return (unsigned)(seq & 0x7fffffffull) | 0x80000000u;
+}
+
+// Workgroups of a bulk push of `len` bytes.  Both sides of a link evaluate
+// this on the same inputs, so the receiver knows how many flags to expect.
+inline int bulk_nwg(long long len, bool same_device) {
+    // ~32 KiB per workgroup across xGMI (enough 16-B stores in flight to
+    // cover the link's bandwidth-delay product), 16 KiB within one GPU.
+    const long long per = same_device ? (16 << 10) : (32 << 10);
+    long long n = (len + per - 1) / per;
+    const long long cap = same_device ? 256 : 128;
+    if (n < 1) n = 1;
+    if (n > cap) n = cap;
+    return (int)n;
+}
+
+// Launchers implemented in mpx_kernels.hip
+hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s);
+hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int* grid_out);
+hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s);
+hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s);
+hipError_t launch_signal(u64* flag, u64 value, hipStream_t s);
+hipError_t launch_wait(const u64* flag, u64 value, Status* st, u64 timeout_ticks, hipStream_t s);
+
+}  // namespace mpx

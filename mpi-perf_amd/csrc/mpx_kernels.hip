@@ -1,0 +1,463 @@
+// mpx_kernels.hip — CDNA4 (gfx950) device code of libmpx.
+//
+// Kernels
+//   k_copy      local HBM copy, 16 B per lane, 4 loads in flight   (config 2)
+//   k_xfer      the reference's three transfer loops as ONE persistent launch
+//               per rank: pushes go straight into the peer's HBM over xGMI,
+//               receives are device-side polls of the rank's mailbox
+//               (do_mpi_benchmark*, /root/reference/mpi_perf.c:66-145)
+//   k_fill      tx fill (memset 'a'/'b', mpi_perf.c:244-251, or a seeded pattern)
+//   k_checksum  order-independent 64-bit payload checksum
+//   k_signal / k_wait   one-lane flag store / bounded poll (SDMA engine)
+//
+// Memory-ordering contract (see DESIGN.md "Hand-off"):
+//  * bulk payload: 16-B buffer stores with sc0|sc1 (system-scope write-through),
+//    every storing wave `s_waitcnt vmcnt(0)`, workgroup barrier, then ONE lane
+//    stores the workgroup's flag with a system-scope relaxed store;
+//  * LL payload (<= 8 KiB, or a 1-byte ack): the data IS the flag — 8-byte
+//    {tag, 4 payload bytes} granules, each written by one system-scope store;
+//  * receivers poll with system-scope relaxed loads (sc0 sc1) and bounded
+//    spins (s_memrealtime deadline); after a timeout every workgroup exits.
+#include "mpx_internal.h"
+
+namespace mpx {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+constexpr u64 kGolden = 0x9E3779B97F4A7C15ull;
+constexpr int kAuxSys = 17;                 // buffer cache policy: sc0 | sc1
+constexpr unsigned kRsrcWord3 = 0x00020000; // raw buffer, 32-bit data format
+
+__device__ __forceinline__ u64 mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+// checksum term of little-endian 64-bit word w at word index k
+__device__ __forceinline__ u64 csum_term(u64 w, u64 k) { return mix64(w + (k + 1) * kGolden); }
+// MPX_FILL_SPLITMIX word k
+__device__ __forceinline__ u64 fill_word(u64 key, u64 k) { return mix64((key ^ k) + kGolden); }
+
+__device__ __forceinline__ u64 ld_sys(const u64* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(u64* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, kRsrcWord3);
+}
+
+// 64-bit sum over the workgroup; result valid in thread 0.
+__device__ __forceinline__ u64 block_sum(u64 v, u64* lds4) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) lds4[wave] = v;
+    __syncthreads();
+    u64 s = 0;
+    if (threadIdx.x == 0) s = lds4[0] + lds4[1] + lds4[2] + lds4[3];
+    __syncthreads();
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// k_copy: dst[0:n) = src[0:n).  n16 = n / 16 vector units; the tail bytes are
+// copied by block 0.  Grid-stride with U independent 16-B loads per lane in
+// flight; nontemporal (streaming) loads and stores: every byte is touched once.
+// ---------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_copy(const v4u* __restrict__ src, v4u* __restrict__ dst,
+                                                size_t n16, unsigned tail) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+        v4u r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) __builtin_nontemporal_store(r[u], dst + i + u * stride);
+    }
+    for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    if (blockIdx.x == 0 && threadIdx.x < tail) {
+        const unsigned char* s8 = reinterpret_cast<const unsigned char*>(src + n16);
+        unsigned char* d8 = reinterpret_cast<unsigned char*>(dst + n16);
+        d8[threadIdx.x] = s8[threadIdx.x];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fill
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_fill(unsigned char* p, size_t n, int pattern, u64 arg) {
+    const size_t nw = n / 8;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    u64* p64 = reinterpret_cast<u64*>(p);
+    const u64 bytew = (arg & 0xff) * 0x0101010101010101ull;
+    for (size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x; k < nw; k += stride)
+        p64[k] = pattern == MPX_FILL_BYTE ? bytew : fill_word(arg, k);
+    const unsigned tail = (unsigned)(n & 7);
+    if (blockIdx.x == 0 && threadIdx.x < tail) {
+        const u64 w = pattern == MPX_FILL_BYTE ? bytew : fill_word(arg, nw);
+        p[nw * 8 + threadIdx.x] = (unsigned char)(w >> (8 * threadIdx.x));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_checksum: *out += sum_k csum_term(word_k, k) over the zero-padded 64-bit
+// words of p[0:n).  Integer adds commute, so the result is bit-exact whatever
+// the order; the host finishes it with ^ mix64(n).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u64 tail_word(const unsigned char* p, size_t off, size_t n) {
+    u64 w = 0;
+    for (size_t b = 0; off + b < n && b < 8; ++b) w |= (u64)p[off + b] << (8 * b);
+    return w;
+}
+
+__global__ __launch_bounds__(kBlock) void k_checksum(const unsigned char* p, size_t n, u64* out) {
+    __shared__ u64 lds4[4];
+    const size_t n16 = n / 16;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const v4u* p16 = reinterpret_cast<const v4u*>(p);
+    u64 acc = 0;
+    for (size_t v = (size_t)blockIdx.x * kBlock + threadIdx.x; v < n16; v += stride) {
+        const v4u x = p16[v];
+        acc += csum_term(((u64)x.y << 32) | x.x, 2 * v);
+        acc += csum_term(((u64)x.w << 32) | x.z, 2 * v + 1);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 2) {
+        const size_t off = n16 * 16 + 8 * threadIdx.x;
+        if (off < n) acc += csum_term(tail_word(p, off, n), off / 8);
+    }
+    const u64 s = block_sum(acc, lds4);
+    if (threadIdx.x == 0 && s) atomicAdd(out, s);
+}
+
+// ---------------------------------------------------------------------------
+// SDMA-engine helpers: one lane stores / polls a mailbox flag.
+// ---------------------------------------------------------------------------
+__global__ void k_signal(u64* flag, u64 v) {
+    if (threadIdx.x == 0) st_sys(flag, v);
+}
+
+__global__ void k_wait(const u64* flag, u64 v, Status* st, u64 timeout_ticks) {
+    if (threadIdx.x != 0) return;
+    const u64 t0 = now_ticks();
+    u64 spins = 0;
+    while (ld_sys(flag) < v) {
+        if ((++spins & 255) == 0 && now_ticks() - t0 > timeout_ticks) {
+            __hip_atomic_store(&st->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_xfer: the transfer loop.  One launch runs all `iters` iterations of one
+// rank's side; the peer runs its own launch on its own GPU at the same time.
+// ---------------------------------------------------------------------------
+struct Loop {
+    const XferArgs& a;
+    int* s_abort;      // LDS: this workgroup gave up
+    u64* lds4;         // LDS scratch for block_sum
+
+    __device__ bool aborted() const { return *s_abort != 0; }
+
+    // Record a timeout: LDS flag for this workgroup, device word for the
+    // others (scratch[1]), host-mapped status for the host.
+    __device__ void give_up(int iter) const {
+        *s_abort = 1;
+        __hip_atomic_store(&a.gbar[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.status->where, (unsigned)iter + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.status->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // every 64 spins: deadline or another workgroup's abort
+    __device__ bool should_stop(u64 spins, u64 t0) const {
+        if ((spins & 63) != 0) return false;
+        if (*s_abort) return true;
+        if (__hip_atomic_load(&a.gbar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+        return now_ticks() - t0 > a.timeout_ticks;
+    }
+
+    __device__ bool is_ll(long long n) const { return a.mode != MPX_MODE_NONBLOCKING && n <= kLLMaxBytes; }
+
+    // ---- send: push n bytes of tx[0:n) into the peer's rx -------------------
+    __device__ void push_ll(long long n, u64 seq) const {
+        if (blockIdx.x != 0) return;
+        const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;   // a 0-byte message is one empty granule
+        const u64 tag = (u64)ll_tag(seq) << 32;
+        u64* g = &a.peer_mb->ll[a.my_slot][0];
+        for (int k = threadIdx.x; k < ng; k += kBlock) {
+            unsigned d;
+            const long long off = 4ll * k;
+            if (off + 4 <= n) {
+                d = *reinterpret_cast<const unsigned*>(a.tx + off);
+            } else {
+                d = 0;
+                for (long long b = 0; off + b < n; ++b) d |= (unsigned)a.tx[off + b] << (8 * b);
+            }
+            st_sys(g + k, tag | d);
+        }
+    }
+
+    __device__ void push_bulk(long long n, u64 seq) const {
+        const int w = blockIdx.x;
+        if (w >= a.nwg) return;
+        const long long chunk = (((n + a.nwg - 1) / a.nwg) + 15) & ~15ll;
+        const long long lo = (long long)w * chunk;
+        const long long hi = lo + chunk < n ? lo + chunk : n;
+        if (lo < hi) {
+            const unsigned bytes = (unsigned)(hi - lo);
+            const __amdgpu_buffer_rsrc_t dst = rsrc(a.peer_rx + lo, bytes);
+            const v4u* src = reinterpret_cast<const v4u*>(a.tx + lo);
+            const int nv = (int)(bytes >> 4);
+            int v = threadIdx.x;
+            for (; v + 3 * kBlock < nv; v += 4 * kBlock) {
+                const v4u r0 = src[v], r1 = src[v + kBlock], r2 = src[v + 2 * kBlock], r3 = src[v + 3 * kBlock];
+                __builtin_amdgcn_raw_buffer_store_b128(r0, dst, v * 16, 0, kAuxSys);
+                __builtin_amdgcn_raw_buffer_store_b128(r1, dst, (v + kBlock) * 16, 0, kAuxSys);
+                __builtin_amdgcn_raw_buffer_store_b128(r2, dst, (v + 2 * kBlock) * 16, 0, kAuxSys);
+                __builtin_amdgcn_raw_buffer_store_b128(r3, dst, (v + 3 * kBlock) * 16, 0, kAuxSys);
+            }
+            for (; v < nv; v += kBlock) __builtin_amdgcn_raw_buffer_store_b128(src[v], dst, v * 16, 0, kAuxSys);
+            const unsigned tail = bytes & 15;
+            if (threadIdx.x < tail) {
+                const unsigned o = (unsigned)nv * 16 + threadIdx.x;
+                __builtin_amdgcn_raw_buffer_store_b8(a.tx[lo + o], dst, o, 0, kAuxSys);
+            }
+        }
+        drain_stores();                 // every storing wave
+        __syncthreads();
+        if (threadIdx.x == 0) st_sys(&a.peer_mb->flag[a.my_slot][w], seq);
+    }
+
+    __device__ void send(long long n, u64 seq) const {
+        if (is_ll(n)) push_ll(n, seq); else push_bulk(n, seq);
+    }
+
+    // ---- receive: wait until the peer's push `seq` of n bytes has landed ----
+    __device__ bool wait_ll(long long n, u64 seq, int iter) const {
+        const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;
+        const unsigned tag = ll_tag(seq);
+        const u64* g = &a.my_mb->ll[a.peer_slot][0];
+        const bool unpack = blockIdx.x == 0;
+        // a multi-granule LL message is only ever received by a 1-WG grid
+        for (int k = threadIdx.x; k < ng; k += kBlock) {
+            const u64 t0 = now_ticks();
+            u64 x, spins = 0;
+            while ((unsigned)((x = ld_sys(g + k)) >> 32) != tag) {
+                if (should_stop(++spins, t0)) { give_up(iter); break; }
+                __builtin_amdgcn_s_sleep(0);
+            }
+            if (*s_abort) break;
+            if (unpack) {
+                const long long off = 4ll * k;
+                const unsigned d = (unsigned)x;
+                if (off + 4 <= n) {
+                    *reinterpret_cast<unsigned*>(a.rx + off) = d;
+                } else {
+                    for (long long b = 0; off + b < n; ++b) a.rx[off + b] = (unsigned char)(d >> (8 * b));
+                }
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
+
+    __device__ bool wait_bulk(u64 seq, int iter) const {
+        if (threadIdx.x < 64) {
+            const u64* f = &a.my_mb->flag[a.peer_slot][0];
+            const u64 t0 = now_ticks();
+            u64 spins = 0;
+            for (;;) {
+                bool ok = true;
+                for (int j = threadIdx.x; j < a.nwg; j += 64) ok &= ld_sys(f + j) >= seq;
+                if (__all(ok)) break;
+                if (should_stop(++spins, t0)) {
+                    if (threadIdx.x == 0) give_up(iter);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
+
+    __device__ bool recv(long long n, u64 seq, int iter) const {
+        return is_ll(n) ? wait_ll(n, seq, iter) : wait_bulk(seq, iter);
+    }
+
+    // ---- check mode: checksum the received payload, then poison it ----------
+    // The poison guarantees the NEXT iteration's checksum only passes if the
+    // next payload really overwrote every byte.
+    __device__ void check(long long n, int iter) const {
+        const u64 poison = 0x5a5a5a5a5a5a5a5aull ^ (u64)iter;
+        u64 acc = 0;
+        if (is_ll(n)) {
+            // unpacked by workgroup 0 with plain stores: same-workgroup reads
+            if (blockIdx.x == 0) {
+                for (long long k = threadIdx.x; 8 * k < n; k += kBlock)
+                    acc += csum_term(tail_word(a.rx, 8 * k, n), k);
+                __syncthreads();
+                for (long long o = threadIdx.x; o < n; o += kBlock) a.rx[o] = (unsigned char)poison;
+            }
+        } else if ((int)blockIdx.x < a.nwg) {
+            // bytes stored by the peer: system-scope acquire, then sc0|sc1 loads
+            if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            drain_stores();
+            __syncthreads();
+            const long long chunk = (((n + a.nwg - 1) / a.nwg) + 15) & ~15ll;
+            const long long lo = (long long)blockIdx.x * chunk;
+            const long long hi = lo + chunk < n ? lo + chunk : n;
+            if (lo < hi) {
+                const unsigned bytes = (unsigned)(hi - lo);
+                const __amdgpu_buffer_rsrc_t r = rsrc(a.rx + lo, bytes);
+                const int nv = (int)(bytes >> 4);
+                const v4u pv = {(unsigned)poison, (unsigned)(poison >> 32), (unsigned)poison, (unsigned)(poison >> 32)};
+                for (int v = threadIdx.x; v < nv; v += kBlock) {
+                    const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, v * 16, 0, kAuxSys);
+                    const u64 k = (u64)(lo / 8) + 2 * (u64)v;
+                    acc += csum_term(((u64)x.y << 32) | x.x, k);
+                    acc += csum_term(((u64)x.w << 32) | x.z, k + 1);
+                    __builtin_amdgcn_raw_buffer_store_b128(pv, r, v * 16, 0, kAuxSys);
+                }
+                const unsigned tail = bytes & 15;   // only the last workgroup
+                if (threadIdx.x < 2 && 8 * threadIdx.x < tail) {
+                    const long long off = lo + (long long)nv * 16 + 8 * threadIdx.x;
+                    u64 w = 0;
+                    for (long long b = 0; b < 8 && off + b < n; ++b) {
+                        const unsigned char c = __builtin_amdgcn_raw_buffer_load_b8(r, (unsigned)(off - lo + b), 0, kAuxSys);
+                        w |= (u64)c << (8 * b);
+                    }
+                    acc += csum_term(w, (u64)off / 8);
+                }
+                __syncthreads();
+                if (threadIdx.x < tail)
+                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)poison, r, (unsigned)nv * 16 + threadIdx.x, 0, kAuxSys);
+            }
+            drain_stores();
+        }
+        const u64 s = block_sum(acc, lds4);
+        if (threadIdx.x == 0 && s) atomicAdd(&a.csum[iter], s);
+    }
+
+    // all workgroups finished check(): the 1-WG ack must not overtake a poison
+    __device__ bool grid_sync(int iter) const {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(&a.gbar[0], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (blockIdx.x == 0) {
+                const u64 want = (u64)gridDim.x * (u64)(iter + 1);
+                const u64 t0 = now_ticks();
+                u64 spins = 0;
+                while (__hip_atomic_load(&a.gbar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                    if (should_stop(++spins, t0)) { give_up(iter); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
+    __shared__ int s_abort;
+    __shared__ u64 lds4[4];
+    if (threadIdx.x == 0) s_abort = 0;
+    __syncthreads();
+    Loop L{a, &s_abort, lds4};
+    const long long n = a.len;
+    u64 txs = a.tx_seq0, rxs = a.rx_seq0;
+    int inflight = 0;
+    for (int i = 0; i < a.iters; ++i) {
+        if (a.mode == MPX_MODE_PINGPONG) {            // mpi_perf.c:70-82
+            if (a.group == 1) {
+                L.send(n, ++txs);                      // Send(tx, B, tag 1)
+                if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 2)
+                if (a.check) L.check(n, i);
+            } else {
+                if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 1)
+                if (a.check) L.check(n, i);
+                L.send(n, ++txs);                      // Send(tx, B, tag 2)
+            }
+        } else if (a.mode == MPX_MODE_UNIDIR) {        // mpi_perf.c:132-144
+            if (a.group == 1) {
+                L.send(n, ++txs);                      // Send(tx, B)
+                if (!L.recv(1, ++rxs, i)) break;       // Recv(rx, 1) — the ack
+                if (a.check) L.check(1, i);
+            } else {
+                if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B)
+                if (a.check) { L.check(n, i); if (!L.grid_sync(i)) break; }
+                L.send(1, ++txs);                      // Send(tx, 1)
+            }
+        } else {                                       // mpi_perf.c:95-124
+            L.send(n, ++txs);                          // Isend + Irecv, slot `inflight`
+            if (inflight == kNbWindow - 1) {
+                // Waitall(255, ...): the receive posted in slot 255 (this
+                // iteration) is not among the 255 waited for (mpi_perf.c:110-111)
+                if (!L.wait_bulk(rxs + i, i)) break;
+                inflight = 0;
+            } else {
+                ++inflight;
+            }
+        }
+    }
+    if (a.mode == MPX_MODE_NONBLOCKING && inflight > 0 && !L.aborted())
+        L.wait_bulk(rxs + a.iters, a.iters - 1);       // final Waitall(inflight)
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_xfer, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int* grid_out) {
+    const size_t n16 = n / 16;
+    const unsigned tail = (unsigned)(n & 15);
+    constexpr int U = 4;
+    size_t grid = (n16 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
+    if (grid > 4096) grid = 4096;     // 16 blocks per CU, grid-stride beyond
+    if (grid < 1) grid = 1;
+    if (grid_out) *grid_out = (int)grid;
+    hipLaunchKernelGGL(k_copy<U>, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const v4u*>(src),
+                       reinterpret_cast<v4u*>(dst), n16, tail);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s) {
+    size_t grid = (n / 8 + kBlock - 1) / kBlock;
+    if (grid > 4096) grid = 4096;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<unsigned char*>(p), n,
+                       pattern, arg);
+    return hipGetLastError();
+}
+
+hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s) {
+    size_t grid = (n / 16 + kBlock - 1) / kBlock;
+    if (grid > 2048) grid = 2048;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_checksum, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const unsigned char*>(p),
+                       n, out_dev);
+    return hipGetLastError();
+}
+
+hipError_t launch_signal(u64* flag, u64 value, hipStream_t s) {
+    hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, s, flag, value);
+    return hipGetLastError();
+}
+
+hipError_t launch_wait(const u64* flag, u64 value, Status* st, u64 timeout_ticks, hipStream_t s) {
+    hipLaunchKernelGGL(k_wait, dim3(1), dim3(64), 0, s, flag, value, st, timeout_ticks);
+    return hipGetLastError();
+}
+
+}  // namespace mpx

@@ -1,0 +1,235 @@
+"""ctypes binding of libmpx (include/mpx.h) for tests and bench.py.
+
+This is plumbing over the C-ABI, not a second implementation: every call goes
+to lib/libmpx.so, and importing this module fails loudly if the library is
+missing (there is no CPU fallback — the CPU restatement lives in oracle/ and is
+only ever used as a checker).
+
+Reference mapping: see include/mpx.h (each entry point cites the
+/root/reference/mpi_perf.c call it replaces).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmpx.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "mpx.h")
+
+# enum values (include/mpx.h)
+OK, ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_TIMEOUT, ERR_RCCL, ERR_UNSUPPORTED, ERR_STATE, ERR_CHECK = range(9)
+ENGINE_KERNEL, ENGINE_SDMA, ENGINE_RCCL = 0, 1, 2
+ENGINES = {"kernel": ENGINE_KERNEL, "sdma": ENGINE_SDMA, "rccl": ENGINE_RCCL}
+MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
+MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": MODE_UNIDIR}
+FILL_BYTE, FILL_SPLITMIX = 0, 1
+PATTERN_SEED = 0x6D70695F70657266
+MAX_RANKS = 16
+RANK_DESC_BYTES = 512
+RCCL_ID_BYTES = 128
+PROTOCOLS = {0: "ll", 1: "bulk", 2: "sdma", 3: "rccl", 4: "copy"}
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("wall_s", C.c_double),
+        ("device_s", C.c_double),
+        ("bytes", C.c_uint64),
+        ("launches", C.c_int32),
+        ("nwg", C.c_int32),
+        ("protocol", C.c_int32),
+        ("check_failures", C.c_int32),
+        ("check_iters", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["protocol"] = PROTOCOLS.get(self.protocol, self.protocol)
+        return d
+
+
+class XferOpts(C.Structure):
+    _fields_ = [
+        ("check", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("expect_checksum", C.c_uint64),
+        ("expect_ack", C.c_uint64),
+        ("timeout_ms", C.c_uint32),
+        ("nwg", C.c_int32),
+    ]
+
+
+def pattern_key(seed: int, src: int, dst: int, it: int) -> int:
+    """mpx_pattern_key (include/mpx.h)."""
+    return (seed ^ (src << 56) ^ (dst << 48) ^ (it << 24)) & 0xFFFFFFFFFFFFFFFF
+
+
+_SIGS = {
+    "mpx_version": (C.c_int, []),
+    "mpx_strerror": (C.c_char_p, [C.c_int]),
+    "mpx_last_error": (C.c_char_p, []),
+    "mpx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "mpx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "mpx_finalize": (C.c_int, [C.c_void_p]),
+    "mpx_alloc": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "mpx_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mpx_fill": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_int, C.c_uint64]),
+    "mpx_checksum": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64)]),
+    "mpx_read": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "mpx_copy": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.POINTER(Timing)]),
+    "mpx_rank_attach": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "mpx_rank_export": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "mpx_rank_import": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "mpx_xfer": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                           C.c_int, C.POINTER(C.c_double)]),
+    "mpx_xfer_ex": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                              C.c_int, C.POINTER(XferOpts), C.POINTER(Timing)]),
+    "mpx_barrier": (C.c_int, [C.c_void_p, C.c_int]),
+    "mpx_rccl_get_unique_id": (C.c_int, [C.c_void_p]),
+    "mpx_rccl_init_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "mpx_rccl_init_all": (C.c_int, [C.c_void_p]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load lib/libmpx.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libmpx not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class MpxError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        L = lib()
+        super().__init__(f"{what}: {L.mpx_strerror(status).decode()} ({L.mpx_last_error().decode()})")
+
+
+def check(status: int, what: str) -> None:
+    if status != OK:
+        raise MpxError(status, what)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().mpx_device_count(C.byref(n)), "mpx_device_count")
+    return n.value
+
+
+@dataclass
+class Buffer:
+    ptr: int
+    dev: int
+    size: int
+
+
+class Context:
+    """Thin object wrapper of an mpx_ctx."""
+
+    def __init__(self, nranks: int, engine: int | str = ENGINE_KERNEL):
+        if isinstance(engine, str):
+            engine = ENGINES[engine]
+        self.L = lib()
+        self.h = C.c_void_p()
+        check(self.L.mpx_init(nranks, engine, C.byref(self.h)), "mpx_init")
+        self.nranks = nranks
+        self.engine = engine
+
+    def close(self) -> None:
+        if self.h:
+            check(self.L.mpx_finalize(self.h), "mpx_finalize")
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # buffers
+    def alloc(self, dev: int, size: int) -> Buffer:
+        p = C.c_void_p()
+        check(self.L.mpx_alloc(self.h, dev, size, C.byref(p)), "mpx_alloc")
+        return Buffer(p.value, dev, size)
+
+    def free(self, b: Buffer) -> None:
+        check(self.L.mpx_free(self.h, C.c_void_p(b.ptr)), "mpx_free")
+
+    def fill(self, b: Buffer, n: int, pattern: int, arg: int) -> None:
+        check(self.L.mpx_fill(self.h, b.dev, C.c_void_p(b.ptr), n, pattern, arg & 0xFFFFFFFFFFFFFFFF), "mpx_fill")
+
+    def checksum(self, b: Buffer, n: int, offset: int = 0) -> int:
+        out = C.c_uint64()
+        check(self.L.mpx_checksum(self.h, b.dev, C.c_void_p(b.ptr + offset), n, C.byref(out)), "mpx_checksum")
+        return out.value
+
+    def read(self, b: Buffer, n: int, offset: int = 0) -> bytes:
+        buf = C.create_string_buffer(max(n, 1))
+        check(self.L.mpx_read(self.h, b.dev, buf, C.c_void_p(b.ptr + offset), n), "mpx_read")
+        return buf.raw[:n]
+
+    def copy(self, dev: int, dst: Buffer, src: Buffer, n: int, iters: int) -> Timing:
+        t = Timing()
+        check(self.L.mpx_copy(self.h, dev, C.c_void_p(dst.ptr), C.c_void_p(src.ptr), n, iters, C.byref(t)), "mpx_copy")
+        return t
+
+    # ranks
+    def attach(self, rank: int, dev: int, tx: Buffer, rx: Buffer, length: int) -> None:
+        check(self.L.mpx_rank_attach(self.h, rank, dev, C.c_void_p(tx.ptr), C.c_void_p(rx.ptr), length),
+              "mpx_rank_attach")
+
+    def export(self, rank: int) -> bytes:
+        buf = C.create_string_buffer(RANK_DESC_BYTES)
+        check(self.L.mpx_rank_export(self.h, rank, buf), "mpx_rank_export")
+        return buf.raw
+
+    def import_rank(self, rank: int, desc: bytes) -> None:
+        buf = C.create_string_buffer(bytes(desc), RANK_DESC_BYTES)
+        check(self.L.mpx_rank_import(self.h, rank, buf), "mpx_rank_import")
+
+    def xfer(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, tx: Buffer, rx: Buffer,
+             length: int, check_payload: bool = False, expect: int = 0, expect_ack: int = 0,
+             timeout_ms: int = 0, nwg: int = 0) -> Timing:
+        o = XferOpts(check=1 if check_payload else 0, expect_checksum=expect, expect_ack=expect_ack,
+                     timeout_ms=timeout_ms, nwg=nwg)
+        t = Timing()
+        st = self.L.mpx_xfer_ex(self.h, mode, group, my_rank, peer_rank, iters, C.c_void_p(tx.ptr),
+                                C.c_void_p(rx.ptr), length, C.byref(o), C.byref(t))
+        check(st, "mpx_xfer_ex")
+        return t
+
+    def rccl_init_all(self) -> None:
+        check(self.L.mpx_rccl_init_all(self.h), "mpx_rccl_init_all")
+
+    def rccl_init_rank(self, rank: int, nranks: int, uid: bytes) -> None:
+        buf = C.create_string_buffer(bytes(uid), RCCL_ID_BYTES)
+        check(self.L.mpx_rccl_init_rank(self.h, rank, nranks, buf), "mpx_rccl_init_rank")
+
+
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(RCCL_ID_BYTES)
+    check(lib().mpx_rccl_get_unique_id(buf), "mpx_rccl_get_unique_id")
+    return buf.raw
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function name include/mpx.h declares (for the export test)."""
+    import re
+
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_]+\s*\*?\s*(mpx_[a-z_0-9]+)\s*\(", txt, flags=re.M)
+    return sorted(set(n for n in names if n != "mpx_pattern_key"))

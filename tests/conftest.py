@@ -1,0 +1,20 @@
+"""pytest configuration: the `gpu` marker, paths, and shared helpers.
+
+`-m "not gpu"` runs here (no GPU): oracle vs golden fixtures, host logic, and
+the C-ABI symbol check.  `-m gpu` runs on an MI355X box and calls libmpx
+through its C-ABI, checking every result against the oracle.
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "mpi-perf_amd")
+for p in (PKG, os.path.dirname(os.path.abspath(__file__))):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")

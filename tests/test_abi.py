@@ -1,0 +1,53 @@
+"""The C-ABI library loads and exports every symbol include/mpx.h declares.
+
+CPU-only: no compute call is made (argument validation that returns before
+touching the GPU is allowed).
+"""
+import ctypes
+import os
+import subprocess
+
+import mpx
+
+
+def test_library_built_in_tree():
+    assert os.path.exists(mpx.LIB_PATH)
+    assert mpx.LIB_PATH.startswith(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def test_every_header_symbol_is_exported():
+    syms = mpx.header_symbols()
+    assert len(syms) >= 20
+    L = ctypes.CDLL(mpx.LIB_PATH)
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    dyn = subprocess.run(["nm", "-D", "--defined-only", mpx.LIB_PATH], capture_output=True, text=True).stdout
+    for s in syms:
+        assert f" T {s}\n" in dyn or f" T {s}" in dyn, s
+
+
+def test_version_and_strerror():
+    L = mpx.lib()
+    assert L.mpx_version() == 1
+    texts = {L.mpx_strerror(i).decode() for i in range(9)}
+    assert len(texts) == 9
+    assert L.mpx_strerror(12345) == b"unknown mpx status"
+
+
+def test_argument_validation_without_gpu():
+    L = mpx.lib()
+    h = ctypes.c_void_p()
+    assert L.mpx_init(0, 0, ctypes.byref(h)) == mpx.ERR_INVALID
+    assert L.mpx_init(mpx.MAX_RANKS + 1, 0, ctypes.byref(h)) == mpx.ERR_INVALID
+    assert L.mpx_init(2, 7, ctypes.byref(h)) == mpx.ERR_INVALID
+    assert L.mpx_finalize(None) == mpx.ERR_INVALID
+    assert L.mpx_xfer(None, 0, 1, 0, 1, 1, None, None, 8, None) == mpx.ERR_INVALID
+    assert L.mpx_rccl_get_unique_id(None) == mpx.ERR_INVALID
+    assert b"NULL" in L.mpx_last_error() or L.mpx_last_error()
+
+
+def test_header_constants_match_binding():
+    txt = open(mpx.HEADER_PATH).read()
+    assert "#define MPX_MAX_RANKS 16" in txt and mpx.MAX_RANKS == 16
+    assert "#define MPX_RANK_DESC_BYTES 512" in txt
+    assert "0x6d70695f70657266ULL" in txt and mpx.PATTERN_SEED == 0x6D70695F70657266

@@ -1,0 +1,253 @@
+"""GPU parity tests of libmpx through its C-ABI (run with -m gpu on an MI355X).
+
+Every result is checked against the oracle (oracle/mpx_oracle.c) or against
+the compiled reference's golden receive accounting (tests/golden).  Pairs run
+as loopback ranks on GPU 0 (two ranks of one process on one device, one host
+thread each) — the same kernel, mailbox protocol and sequence bookkeeping the
+cross-GPU path uses, with the peer's HBM being local HBM.
+"""
+import threading
+
+import pytest
+
+import mpx
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 7, 8, 15, 16, 17, 255, 4095, 4096, 65537, (1 << 20) + 3, (64 << 20) + 13]
+GOLDEN = {c["name"]: c for c in O.golden()["cases"]}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = mpx.Context(8, "kernel")
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("pattern", [mpx.FILL_BYTE, mpx.FILL_SPLITMIX])
+def test_fill_and_checksum_match_oracle(ctx, n, pattern):
+    arg = ord("a") if pattern == mpx.FILL_BYTE else mpx.pattern_key(mpx.PATTERN_SEED, 1, 2, 3)
+    b = ctx.alloc(0, max(n, 1))
+    try:
+        ctx.fill(b, n, pattern, arg)
+        want = O.pattern_checksum(n, pattern, arg)
+        assert ctx.checksum(b, n) == want
+        if n <= 4096:
+            assert ctx.read(b, n) == O.fill(n, pattern, arg)
+    finally:
+        ctx.free(b)
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_copy_kernel_matches_oracle(ctx, n):
+    key = mpx.pattern_key(mpx.PATTERN_SEED, 0, 0, n & 0xFFFF)
+    src, dst = ctx.alloc(0, max(n, 1)), ctx.alloc(0, max(n, 1) + 64)
+    try:
+        ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
+        ctx.fill(dst, n + 64, mpx.FILL_BYTE, 0xEE)
+        t = ctx.copy(0, dst, src, n, 2)
+        assert ctx.checksum(dst, n) == O.pattern_checksum(n, mpx.FILL_SPLITMIX, key)
+        # nothing written past the end
+        assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
+        assert t.bytes == 2 * n
+        assert t.launches == (2 if n else 0)
+    finally:
+        ctx.free(src)
+        ctx.free(dst)
+
+
+# --------------------------------------------------------------------------
+# loopback pairs
+# --------------------------------------------------------------------------
+class Pairs:
+    """`npairs` pairs of loopback ranks on GPU 0: ranks [0,np) are group 1,
+    ranks [np, 2np) group 0, rank k paired with np+k (the -p ppn layout)."""
+
+    def __init__(self, engine, npairs, cap, fill="compat"):
+        self.c = mpx.Context(2 * npairs, engine)
+        self.np = npairs
+        self.cap = cap
+        self.bufs = []
+        for r in range(2 * npairs):
+            tx, rx = self.c.alloc(0, cap), self.c.alloc(0, cap)
+            if fill == "compat":   # mpi_perf.c:244-251: group 0 'a', group 1 'b'
+                self.c.fill(tx, cap, mpx.FILL_BYTE, ord("b") if r < npairs else ord("a"))
+            else:
+                self.c.fill(tx, cap, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, r, 0, 0))
+            self.c.fill(rx, cap, mpx.FILL_BYTE, 0)
+            self.c.attach(r, 0, tx, rx, cap)
+            self.bufs.append((tx, rx))
+
+    def peer(self, r):
+        return r + self.np if r < self.np else r - self.np
+
+    def group(self, r):
+        return 1 if r < self.np else 0
+
+    def expect(self, r, n):
+        tx = self.bufs[self.peer(r)][0]
+        return self.c.checksum(tx, n), self.c.checksum(tx, min(n, 1))
+
+    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None):
+        ranks = list(range(2 * self.np)) if ranks is None else ranks
+        exp = {r: self.expect(r, n) for r in ranks}
+        out, errs = {}, {}
+
+        def side(r):
+            try:
+                out[r] = self.c.xfer(mode, self.group(r), r, self.peer(r), iters, self.bufs[r][0], self.bufs[r][1],
+                                     n, check_payload=check, expect=exp[r][0], expect_ack=exp[r][1],
+                                     timeout_ms=timeout_ms)
+            except mpx.MpxError as e:
+                errs[r] = e
+
+        th = [threading.Thread(target=side, args=(r,)) for r in ranks]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return out, errs
+
+    def close(self):
+        self.c.close()
+
+
+MODES = [mpx.MODE_PINGPONG, mpx.MODE_NONBLOCKING, mpx.MODE_UNIDIR]
+PAIR_SIZES = [0, 1, 8, 4097, 8192, 8193, 65541, 456131, 4 << 20]
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+@pytest.mark.parametrize("mode", MODES)
+def test_loopback_pair_every_payload(engine, mode):
+    P = Pairs(engine, 1, 4 << 20)
+    try:
+        for n in PAIR_SIZES:
+            iters = 300 if (mode == mpx.MODE_NONBLOCKING and n <= 65541) else 7
+            out, errs = P.run(mode, n, iters)
+            assert not errs, (n, errs)
+            for r in (0, 1):
+                t = out[r]
+                if mode != mpx.MODE_NONBLOCKING:
+                    assert t.check_iters == iters and t.check_failures == 0, (n, r)
+                assert t.bytes == n * iters * (1 if mode == mpx.MODE_UNIDIR else 2)
+            # the delivered bytes: G0 rx = G1's tx; G1 rx = G0's tx (all of it,
+            # or its first byte for unidir's 1-byte ack, mpi_perf.c:137,142)
+            for r in (0, 1):
+                m = 1 if (mode == mpx.MODE_UNIDIR and r == 0 and n) else n
+                want = P.c.checksum(P.bufs[P.peer(r)][0], m)
+                assert P.c.checksum(P.bufs[r][1], m) == want, (n, r)
+    finally:
+        P.close()
+
+
+@pytest.mark.parametrize("name", ["pingpong_p2_b456131_i3", "unidir_p2_b4096_i7", "pingpong_p4_b8_i10",
+                                  "unidir_p4_b456131_i3", "nonblocking_p2_b4096_i7", "defaults_unidir"])
+def test_receive_digest_matches_reference(name):
+    """Runs the golden case's configuration (pairs, mode, B, iters, runs) on the
+    GPU with every payload checksummed, and compares each rank's receive
+    digest with what the compiled reference's ranks received."""
+    c = GOLDEN[name]
+    a = c["args"]
+    ppn = c["ppn"]
+    runs = int(a[a.index("-r") + 1])
+    iters = int(a[a.index("-i") + 1]) if "-i" in a else 10
+    B = int(a[a.index("-b") + 1]) if "-b" in a else 456131
+    mode = mpx.MODE_UNIDIR if "-u" in a else (mpx.MODE_NONBLOCKING if "-x" in a else mpx.MODE_PINGPONG)
+    P = Pairs("kernel", ppn, max(B, 1))
+    try:
+        digest = {r: [0, 0, 0] for r in range(2 * ppn)}
+        for _ in range(runs):
+            out, errs = P.run(mode, B, iters)
+            assert not errs, errs
+            for r in range(2 * ppn):
+                ack = mode == mpx.MODE_UNIDIR and P.group(r) == 1
+                m = min(B, 1) if ack else B
+                if mode == mpx.MODE_NONBLOCKING:
+                    k = O.lib().oracle_nb_waited(iters)
+                    one = P.c.checksum(P.bufs[r][1], m)   # every receive carries the same bytes
+                else:
+                    assert out[r].check_failures == 0 and out[r].check_iters == iters
+                    k = iters
+                    one = P.expect(r, m)[0]
+                digest[r][0] += k
+                digest[r][1] += k * m
+                digest[r][2] = (digest[r][2] + k * one) & 0xFFFFFFFFFFFFFFFF
+        for r in range(2 * ppn):
+            ref = c["shim"][str(r)]
+            assert digest[r] == [ref["recv_done"], ref["recv_bytes"], ref["recv_digest"]], r
+    finally:
+        P.close()
+
+
+def test_sequence_state_across_runs_and_sizes():
+    """One link reused across protocols: LL -> bulk -> LL -> nb -> unidir."""
+    P = Pairs("kernel", 1, 1 << 20, fill="pattern")
+    try:
+        for mode, n, it in [(0, 8, 5), (0, 100000, 3), (2, 4096, 9), (1, 1000, 600), (2, 300000, 4),
+                            (0, 1, 11), (1, 1 << 20, 3), (2, 0, 5)]:
+            out, errs = P.run(mode, n, it)
+            assert not errs, (mode, n, errs)
+    finally:
+        P.close()
+
+
+def test_concurrent_pairs():
+    P = Pairs("kernel", 4, 456131, fill="pattern")
+    try:
+        for mode in MODES:
+            out, errs = P.run(mode, 456131, 5)
+            assert not errs, errs
+    finally:
+        P.close()
+
+
+def test_timeout_when_peer_never_runs():
+    P = Pairs("kernel", 1, 65536)
+    try:
+        out, errs = P.run(mpx.MODE_PINGPONG, 65536, 3, timeout_ms=300, ranks=[0])
+        assert 0 in errs and errs[0].status == mpx.ERR_TIMEOUT
+        # the link state is unknown afterwards: further transfers are refused
+        out, errs = P.run(mpx.MODE_PINGPONG, 8, 1, timeout_ms=300, ranks=[0])
+        assert errs[0].status == mpx.ERR_STATE
+    finally:
+        P.close()
+
+
+def test_check_mode_detects_missing_payload():
+    """Tell the receiver to expect a different payload: every iteration fails."""
+    P = Pairs("kernel", 1, 65536)
+    try:
+        out, errs = {}, {}
+        exp1 = P.expect(1, 65536)
+
+        def side(r, bad):
+            try:
+                out[r] = P.c.xfer(mpx.MODE_PINGPONG, P.group(r), r, P.peer(r), 4, P.bufs[r][0], P.bufs[r][1], 65536,
+                                  check_payload=True, expect=(exp1[0] ^ 1) if bad else P.expect(r, 65536)[0],
+                                  timeout_ms=5000)
+            except mpx.MpxError as e:
+                errs[r] = e
+
+        th = [threading.Thread(target=side, args=(0, False)), threading.Thread(target=side, args=(1, True))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert 1 in errs and errs[1].status == mpx.ERR_CHECK
+    finally:
+        P.close()
+
+
+def test_invalid_arguments(ctx):
+    b = ctx.alloc(0, 64)
+    try:
+        with pytest.raises(mpx.MpxError) as e:
+            ctx.attach(0, 0, b, b, 1 << 30)           # longer than the allocation
+        assert e.value.status == mpx.ERR_INVALID
+        with pytest.raises(mpx.MpxError):
+            ctx.xfer(0, 1, 0, 1, 1, b, b, 8)          # rank 0 not attached
+    finally:
+        ctx.free(b)
