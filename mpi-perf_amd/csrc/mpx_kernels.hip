@@ -294,8 +294,11 @@ struct Loop {
     // ---- check mode: checksum the received payload, then poison it ----------
     // The poison guarantees the NEXT iteration's checksum only passes if the
     // next payload really overwrote every byte.
+    // The last iteration is not poisoned: rx ends holding the last payload,
+    // as the reference's rx does.
     __device__ void check(long long n, int iter) const {
         const u64 poison = 0x5a5a5a5a5a5a5a5aull ^ (u64)iter;
+        const bool last = iter + 1 == a.iters;
         u64 acc = 0;
         if (is_ll(n)) {
             // unpacked by workgroup 0 with plain stores: same-workgroup reads
@@ -303,7 +306,8 @@ struct Loop {
                 for (long long k = threadIdx.x; 8 * k < n; k += kBlock)
                     acc += csum_term(tail_word(a.rx, 8 * k, n), k);
                 __syncthreads();
-                for (long long o = threadIdx.x; o < n; o += kBlock) a.rx[o] = (unsigned char)poison;
+                if (!last)
+                    for (long long o = threadIdx.x; o < n; o += kBlock) a.rx[o] = (unsigned char)poison;
             }
         } else if ((int)blockIdx.x < a.nwg) {
             // bytes stored by the peer: system-scope acquire, then sc0|sc1 loads
@@ -323,7 +327,7 @@ struct Loop {
                     const u64 k = (u64)(lo / 8) + 2 * (u64)v;
                     acc += csum_term(((u64)x.y << 32) | x.x, k);
                     acc += csum_term(((u64)x.w << 32) | x.z, k + 1);
-                    __builtin_amdgcn_raw_buffer_store_b128(pv, r, v * 16, 0, kAuxSys);
+                    if (!last) __builtin_amdgcn_raw_buffer_store_b128(pv, r, v * 16, 0, kAuxSys);
                 }
                 const unsigned tail = bytes & 15;   // only the last workgroup
                 if (threadIdx.x < 2 && 8 * threadIdx.x < tail) {
@@ -336,7 +340,7 @@ struct Loop {
                     acc += csum_term(w, (u64)off / 8);
                 }
                 __syncthreads();
-                if (threadIdx.x < tail)
+                if (!last && threadIdx.x < tail)
                     __builtin_amdgcn_raw_buffer_store_b8((unsigned char)poison, r, (unsigned)nv * 16 + threadIdx.x, 0, kAuxSys);
             }
             drain_stores();

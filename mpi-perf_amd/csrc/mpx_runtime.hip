@@ -104,6 +104,7 @@ struct Rank {
     u64* scratch = nullptr;        // [0] grid barrier, [1] abort (local ranks)
     u64* csum = nullptr;           // per-iteration checksums (device)
     size_t csum_cap = 0;
+    std::vector<void*> retired;    // outgrown csum arrays (freed at finalize)
     u64 tx_seq[MPX_MAX_RANKS] = {};
     u64 rx_seq[MPX_MAX_RANKS] = {};
     ncclComm_t comm = nullptr;
@@ -138,6 +139,7 @@ struct mpx_ctx {
     std::map<int, hipStream_t> dev_stream;     // utility stream per device
     std::map<int, u64*> dev_tmp;               // 8-byte device scratch per device
     std::vector<void*> ipc_opened;             // to close on finalize
+    std::mutex util_mu;                        // fill / checksum / copy share dev_stream + dev_tmp
     int import_dev = -1;
     // barrier (mpx_barrier)
     std::mutex bmu;
@@ -177,39 +179,103 @@ int check_dev(int dev) {
 // Allocate the rank's mailbox; prefer uncached device memory (every access
 // goes to memory, so polls see xGMI stores), then fine-grained, then coarse.
 // The kind must also be IPC-exportable for multi-process use.
+// MPX_MAILBOX=uncached|fine|coarse forces one kind (diagnostics).
 int alloc_mailbox(Rank& rk) {
     const unsigned flags[2] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
-    for (int k = 0; k < 2; ++k) {
+    const char* force = getenv("MPX_MAILBOX");
+    int first = 0, last = 1;
+    if (force && !strcmp(force, "fine")) first = 1;
+    if (force && !strcmp(force, "coarse")) first = 2;
+    if (force && !strcmp(force, "uncached")) last = 0;
+    for (int k = first; k <= last; ++k) {
         void* p = nullptr;
         if (hipExtMallocWithFlags(&p, sizeof(Mailbox), flags[k]) != hipSuccess) {
             (void)hipGetLastError();
             continue;
         }
         hipIpcMemHandle_t h;
-        if (hipIpcGetMemHandle(&h, p) != hipSuccess) {
+        const hipError_t e = hipIpcGetMemHandle(&h, p);
+        if (getenv("MPX_DEBUG"))
+            fprintf(stderr, "[mpx] mailbox kind %d alloc ok, ipc handle: %s\n", k, hipGetErrorString(e));
+        if (e != hipSuccess && !getenv("MPX_MAILBOX")) {
             (void)hipGetLastError();
             (void)hipFree(p);
             continue;
         }
+        (void)hipGetLastError();
         rk.mb = static_cast<Mailbox*>(p);
         rk.mb_kind = k;
         return MPX_OK;
     }
     void* p = nullptr;
     HIPCK(hipMalloc(&p, sizeof(Mailbox)));
+    if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] mailbox kind 2 (coarse hipMalloc)\n");
     rk.mb = static_cast<Mailbox*>(p);
     rk.mb_kind = kMbCoarse;
     return MPX_OK;
 }
 
+// Grows the checksum array without hipFree: hipFree waits for the whole
+// device, i.e. for other ranks' spinning transfer kernels on the same GPU,
+// which may be waiting for this rank.  Retired arrays are freed at finalize.
 int ensure_csum(Rank& rk, int iters) {
     if ((size_t)iters <= rk.csum_cap) return MPX_OK;
-    if (rk.csum) HIPCK(hipFree(rk.csum));
+    if (rk.csum) rk.retired.push_back(rk.csum);
     rk.csum = nullptr;
     size_t cap = 1024;
     while (cap < (size_t)iters) cap *= 2;
     HIPCK(hipMalloc(&rk.csum, cap * sizeof(u64)));
     rk.csum_cap = cap;
+    return MPX_OK;
+}
+
+// A rank's stream must own its hardware queue.  The two halves of a pair
+// are co-dependent persistent kernels; when both ranks live on one GPU and
+// HIP multiplexes their streams onto one of its GPU_MAX_HW_QUEUES shared
+// queues, the second kernel waits behind the first and both time out.  A
+// stream created with a CU mask is never placed on a shared queue, so every
+// rank stream is created with a mask that enables all CUs.
+// MPX_STREAM=plain falls back to an ordinary non-blocking stream.
+//
+// Destroying a CU-masked stream was observed to leave later HIP calls of the
+// process hanging (gfx950 / ROCm 7.2), so these streams are never destroyed:
+// finalize returns them to a process-wide pool and the next attach reuses them.
+std::mutex g_pool_mu;
+std::map<int, std::vector<hipStream_t>> g_stream_pool;
+
+bool plain_streams() {
+    const char* kind = getenv("MPX_STREAM");
+    return kind && !strcmp(kind, "plain");
+}
+
+void release_rank_stream(int dev, hipStream_t s) {
+    if (plain_streams()) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_stream_pool[dev].push_back(s);
+}
+
+int create_rank_stream(int dev, hipStream_t* s) {
+    if (plain_streams()) {
+        HIPCK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+        return MPX_OK;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        auto& v = g_stream_pool[dev];
+        if (!v.empty()) {
+            *s = v.back();
+            v.pop_back();
+            return MPX_OK;
+        }
+    }
+    hipDeviceProp_t prop;
+    HIPCK(hipGetDeviceProperties(&prop, dev));
+    const int words = (prop.multiProcessorCount + 31) / 32;
+    std::vector<uint32_t> mask((size_t)words, 0xffffffffu);
+    HIPCK(hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask.data()));
     return MPX_OK;
 }
 
@@ -313,10 +379,11 @@ struct SdmaOps {
 
 // check mode for the stream engines: checksum the received bytes into
 // csum[i], then poison them — stream-ordered before the next push.
-int stream_check(Rank& me, long long n, int i) {
+int stream_check(Rank& me, long long n, int i, int iters) {
     if (n <= 0) return MPX_OK;
     HIPCK(launch_checksum(me.rx, (size_t)n, me.csum + i, me.stream));
-    HIPCK(launch_fill(me.rx, (size_t)n, MPX_FILL_BYTE, (0x5a ^ i) & 0xff, me.stream));
+    if (i + 1 < iters)   // the last payload stays in rx, as in the reference
+        HIPCK(launch_fill(me.rx, (size_t)n, MPX_FILL_BYTE, (0x5a ^ i) & 0xff, me.stream));
     return MPX_OK;
 }
 
@@ -337,21 +404,21 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
             if (group == 1) {
                 TRY(op.push(len, ++txs));
                 TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, len, i));
+                if (check) TRY(stream_check(me, len, i, iters));
             } else {
                 TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, len, i));
+                if (check) TRY(stream_check(me, len, i, iters));
                 TRY(op.push(len, ++txs));
             }
         } else if (mode == MPX_MODE_UNIDIR) {
             if (group == 1) {
                 TRY(op.push(len, ++txs));
                 TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, 1, i));
+                if (check) TRY(stream_check(me, 1, i, iters));
             } else {
                 TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, len, i));
-                TRY(op.push(len > 0 ? 1 : 0, ++txs));
+                if (check) TRY(stream_check(me, len, i, iters));
+                TRY(op.push(1, ++txs));                  // Send(tx, 1): always one byte
             }
         } else {
             TRY(op.push(len, ++txs));
@@ -401,10 +468,10 @@ int run_rccl(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
             if (group == 1) {
                 NCCLCK(ncclSend(me.tx, n, ncclChar, peer_rank, me.comm, me.stream));
                 NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
-                if (check) TRY(stream_check(me, len, i));
+                if (check) TRY(stream_check(me, len, i, iters));
             } else {
                 NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
-                if (check) TRY(stream_check(me, len, i));
+                if (check) TRY(stream_check(me, len, i, iters));
                 NCCLCK(ncclSend(me.tx, n, ncclChar, peer_rank, me.comm, me.stream));
             }
             launches += 2;
@@ -412,10 +479,10 @@ int run_rccl(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
             if (group == 1) {
                 NCCLCK(ncclSend(me.tx, n, ncclChar, peer_rank, me.comm, me.stream));
                 NCCLCK(ncclRecv(me.rx, 1, ncclChar, peer_rank, me.comm, me.stream));
-                if (check) TRY(stream_check(me, 1, i));
+                if (check) TRY(stream_check(me, 1, i, iters));
             } else {
                 NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
-                if (check) TRY(stream_check(me, len, i));
+                if (check) TRY(stream_check(me, len, i, iters));
                 NCCLCK(ncclSend(me.tx, 1, ncclChar, peer_rank, me.comm, me.stream));
             }
             launches += 2;
@@ -487,33 +554,58 @@ int mpx_init(int nranks, int engine, mpx_ctx** out) {
     return MPX_OK;
 }
 
+#define DBG(...) \
+    do { if (getenv("MPX_DEBUG")) { fprintf(stderr, "[mpx] " __VA_ARGS__); fflush(stderr); } } while (0)
+
 int mpx_finalize(mpx_ctx* ctx) {
     if (!ctx) return fail(MPX_ERR_INVALID, "ctx is NULL");
+    // Teardown order matters: every stream is drained and every allocation
+    // freed BEFORE any stream is destroyed — hipFree after destroying a
+    // CU-masked stream (create_rank_stream) was observed to hang on gfx950 /
+    // ROCm 7.2.
     for (int i = 0; i < MPX_MAX_RANKS; ++i) {
         Rank& rk = ctx->r[i];
         if (rk.comm) (void)ncclCommDestroy(rk.comm);
-        if (rk.local) {
+        rk.comm = nullptr;
+        if (rk.local && rk.stream) {
             DeviceGuard g(rk.dev);
-            if (rk.stream) (void)hipStreamSynchronize(rk.stream);
-            if (rk.ev0) (void)hipEventDestroy(rk.ev0);
-            if (rk.ev1) (void)hipEventDestroy(rk.ev1);
-            if (rk.stream) (void)hipStreamDestroy(rk.stream);
-            if (rk.mb) (void)hipFree(rk.mb);
-            if (rk.scratch) (void)hipFree(rk.scratch);
-            if (rk.csum) (void)hipFree(rk.csum);
-            if (rk.status) (void)hipHostFree(rk.status);
+            (void)hipStreamSynchronize(rk.stream);
         }
     }
+    DBG("finalize: streams drained\n");
     for (void* p : ctx->ipc_opened) (void)hipIpcCloseMemHandle(p);
-    for (auto& kv : ctx->dev_stream) {
-        DeviceGuard g(kv.first);
-        (void)hipStreamDestroy(kv.second);
-        (void)hipFree(ctx->dev_tmp[kv.first]);
+    for (int i = 0; i < MPX_MAX_RANKS; ++i) {
+        Rank& rk = ctx->r[i];
+        if (!rk.local) continue;
+        DeviceGuard g(rk.dev);
+        if (rk.mb) (void)hipFree(rk.mb);
+        if (rk.scratch) (void)hipFree(rk.scratch);
+        if (rk.csum) (void)hipFree(rk.csum);
+        for (void* q : rk.retired) (void)hipFree(q);
+        if (rk.status) (void)hipHostFree(rk.status);
     }
     for (auto& kv : ctx->allocs) {
         DeviceGuard g(kv.second.dev);
         (void)hipFree(reinterpret_cast<void*>(kv.first));
     }
+    for (auto& kv : ctx->dev_tmp) {
+        DeviceGuard g(kv.first);
+        (void)hipFree(kv.second);
+    }
+    DBG("finalize: memory freed\n");
+    for (int i = 0; i < MPX_MAX_RANKS; ++i) {
+        Rank& rk = ctx->r[i];
+        if (!rk.local) continue;
+        DeviceGuard g(rk.dev);
+        if (rk.ev0) (void)hipEventDestroy(rk.ev0);
+        if (rk.ev1) (void)hipEventDestroy(rk.ev1);
+        if (rk.stream) release_rank_stream(rk.dev, rk.stream);
+    }
+    for (auto& kv : ctx->dev_stream) {
+        DeviceGuard g(kv.first);
+        (void)hipStreamDestroy(kv.second);
+    }
+    DBG("finalize: done\n");
     delete ctx;
     return MPX_OK;
 }
@@ -562,6 +654,7 @@ int mpx_fill(mpx_ctx* ctx, int dev, void* ptr, size_t n, int pattern, uint64_t a
     if (!n) return MPX_OK;
     hipStream_t s;
     TRY(util_stream(ctx, dev, &s));
+    std::lock_guard<std::mutex> ul(ctx->util_mu);
     DeviceGuard g(dev);
     HIPCK(launch_fill(ptr, n, pattern, arg, s));
     HIPCK(hipStreamSynchronize(s));
@@ -573,6 +666,7 @@ int mpx_checksum(mpx_ctx* ctx, int dev, const void* ptr, size_t n, uint64_t* out
     TRY(check_dev(dev));
     hipStream_t s;
     TRY(util_stream(ctx, dev, &s));
+    std::lock_guard<std::mutex> ul(ctx->util_mu);
     u64* tmp = ctx->dev_tmp[dev];
     DeviceGuard g(dev);
     u64 raw = 0;
@@ -590,8 +684,12 @@ int mpx_read(mpx_ctx* ctx, int dev, void* host_dst, const void* dev_src, size_t 
     if (!ctx || ((!host_dst || !dev_src) && n)) return fail(MPX_ERR_INVALID, "NULL argument");
     TRY(check_dev(dev));
     if (!n) return MPX_OK;
+    hipStream_t s;
+    TRY(util_stream(ctx, dev, &s));
+    std::lock_guard<std::mutex> ul(ctx->util_mu);
     DeviceGuard g(dev);
-    HIPCK(hipMemcpy(host_dst, dev_src, n, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpyAsync(host_dst, dev_src, n, hipMemcpyDeviceToHost, s));
+    HIPCK(hipStreamSynchronize(s));
     return MPX_OK;
 }
 
@@ -603,6 +701,7 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     memset(t, 0, sizeof *t);
     hipStream_t s;
     TRY(util_stream(ctx, dev, &s));
+    std::lock_guard<std::mutex> ul(ctx->util_mu);
     DeviceGuard g(dev);
     hipEvent_t e0, e1;
     HIPCK(hipEventCreate(&e0));
@@ -629,17 +728,17 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
 int mpx_rank_attach(mpx_ctx* ctx, int rank, int dev, void* tx, void* rx, size_t len) {
     if (!ctx) return fail(MPX_ERR_INVALID, "ctx is NULL");
     if (rank < 0 || rank >= ctx->nranks) return fail(MPX_ERR_INVALID, "rank %d not in [0,%d)", rank, ctx->nranks);
-    if ((!tx || !rx) && len) return fail(MPX_ERR_INVALID, "NULL tx/rx");
+    if (!tx || !rx) return fail(MPX_ERR_INVALID, "NULL tx/rx");
     if (len > 0x7fffffffull) return fail(MPX_ERR_INVALID, "len %zu exceeds the reference's int buff_len", len);
     TRY(check_dev(dev));
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (ctx->r[rank].local || ctx->r[rank].imported) return fail(MPX_ERR_STATE, "rank %d already registered", rank);
         auto it = ctx->allocs.find(reinterpret_cast<uintptr_t>(rx));
-        if (len && (it == ctx->allocs.end() || it->second.dev != dev || it->second.bytes < len))
+        if (it == ctx->allocs.end() || it->second.dev != dev || it->second.bytes < len)
             return fail(MPX_ERR_INVALID, "rx must be an mpx_alloc base on device %d of >= %zu bytes", dev, len);
         auto jt = ctx->allocs.find(reinterpret_cast<uintptr_t>(tx));
-        if (len && (jt == ctx->allocs.end() || jt->second.dev != dev || jt->second.bytes < len))
+        if (jt == ctx->allocs.end() || jt->second.dev != dev || jt->second.bytes < len)
             return fail(MPX_ERR_INVALID, "tx must be an mpx_alloc base on device %d of >= %zu bytes", dev, len);
     }
     DeviceGuard g(dev);
@@ -652,15 +751,15 @@ int mpx_rank_attach(mpx_ctx* ctx, int rank, int dev, void* tx, void* rx, size_t 
     rk.len = len;
     HIPCK(hipDeviceGetPCIBusId(rk.bus_id, sizeof rk.bus_id, dev));
     TRY(alloc_mailbox(rk));
-    HIPCK(hipMemset(rk.mb, 0, sizeof(Mailbox)));
-    HIPCK(hipStreamCreateWithFlags(&rk.stream, hipStreamNonBlocking));
+    TRY(create_rank_stream(dev, &rk.stream));
+    HIPCK(hipMemsetAsync(rk.mb, 0, sizeof(Mailbox), rk.stream));
     HIPCK(hipEventCreate(&rk.ev0));
     HIPCK(hipEventCreate(&rk.ev1));
     HIPCK(hipHostMalloc(reinterpret_cast<void**>(&rk.status), sizeof(Status), hipHostMallocCoherent | hipHostMallocMapped));
     memset(rk.status, 0, sizeof(Status));
     HIPCK(hipMalloc(&rk.scratch, 4 * sizeof(u64)));
     TRY(ensure_csum(rk, 1024));
-    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipStreamSynchronize(rk.stream));
 
     std::lock_guard<std::mutex> lk(ctx->mu);
     // peer access between this rank's GPU and every other local rank's GPU
@@ -699,7 +798,7 @@ int mpx_rank_export(mpx_ctx* ctx, int rank, void* desc) {
     memcpy(d.bus_id, rk.bus_id, sizeof d.bus_id);
     gethostname(d.host, sizeof d.host - 1);
     DeviceGuard g(rk.dev);
-    if (rk.len) HIPCK(hipIpcGetMemHandle(&d.rx_handle, rk.rx));
+    HIPCK(hipIpcGetMemHandle(&d.rx_handle, rk.rx));
     HIPCK(hipIpcGetMemHandle(&d.mb_handle, rk.mb));
     memset(desc, 0, MPX_RANK_DESC_BYTES);
     memcpy(desc, &d, sizeof d);
@@ -729,11 +828,9 @@ int mpx_rank_import(mpx_ctx* ctx, int rank, const void* desc) {
     HIPCK(hipIpcOpenMemHandle(&p, d.mb_handle, hipIpcMemLazyEnablePeerAccess));
     ctx->ipc_opened.push_back(p);
     rk.mb = static_cast<Mailbox*>(p);
-    if (d.len) {
-        HIPCK(hipIpcOpenMemHandle(&p, d.rx_handle, hipIpcMemLazyEnablePeerAccess));
-        ctx->ipc_opened.push_back(p);
-        rk.rx = static_cast<unsigned char*>(p);
-    }
+    HIPCK(hipIpcOpenMemHandle(&p, d.rx_handle, hipIpcMemLazyEnablePeerAccess));
+    ctx->ipc_opened.push_back(p);
+    rk.rx = static_cast<unsigned char*>(p);
     ctx->r[rank] = rk;
     return MPX_OK;
 }
@@ -771,9 +868,12 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     t->bytes = (uint64_t)buff_len * (uint64_t)iters * (mode == MPX_MODE_UNIDIR ? 1u : 2u);
     if (check && mode != MPX_MODE_NONBLOCKING && iters > 0) {
         std::vector<u64> raw((size_t)iters);
-        HIPCK(hipMemcpy(raw.data(), me.csum, (size_t)iters * sizeof(u64), hipMemcpyDeviceToHost));
+        // the rank's own stream: a null-stream copy would wait for every
+        // blocking stream of the device, i.e. for other pairs' kernels
+        HIPCK(hipMemcpyAsync(raw.data(), me.csum, (size_t)iters * sizeof(u64), hipMemcpyDeviceToHost, me.stream));
+        HIPCK(hipStreamSynchronize(me.stream));
         const bool ack = mode == MPX_MODE_UNIDIR && my_group == 1;
-        const u64 n = ack ? (buff_len > 0 ? 1 : 0) : (u64)buff_len;
+        const u64 n = ack ? 1 : (u64)buff_len;   // the ack is always 1 byte (mpi_perf.c:137,142)
         const u64 want = ack ? opts->expect_ack : opts->expect_checksum;
         int bad = 0;
         for (int i = 0; i < iters; ++i)
