@@ -153,7 +153,10 @@ def main() -> None:
     import torch
     import mpx
 
-    torch.cuda.set_device(local)
+    # MPX_BENCH_ONE_GPU=1: rehearse the N>1 path with every rank on GPU 0
+    # (two processes on one card share it; the IPC + mailbox path is the same)
+    dev = 0 if os.environ.get("MPX_BENCH_ONE_GPU") else local
+    torch.cuda.set_device(dev)
     dist = None
     if not one:
         import torch.distributed as dist
@@ -189,7 +192,7 @@ def main() -> None:
         algo = 2 * nbytes   # read B + write B per launch
         achieved = algo / per_launch / 1e9
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None, kernel="k_copy<4>",
+                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None, kernel="k_copy<2,nt,nt,contig>",
                     avg_launch_us=round(per_launch * 1e6, 2), algorithmic_bytes_per_launch=algo)
         prof = traffic_from_profile(workload)
         if prof and prof.get("bytes") == nbytes:
@@ -208,9 +211,9 @@ def main() -> None:
         from mpx.schedule import all_pairs_rounds, round_role
         workload = "all_pairs_rounds_unidir"
         c = mpx.Context(world, args.engine)
-        tx, rx = c.alloc(local, nbytes), c.alloc(local, nbytes)
+        tx, rx = c.alloc(dev, nbytes), c.alloc(dev, nbytes)
         c.fill(tx, nbytes, mpx.FILL_BYTE, ord("b"))
-        c.attach(rank, local, tx, rx, nbytes)
+        c.attach(rank, dev, tx, rx, nbytes)
         descs = [None] * world
         dist.all_gather_object(descs, c.export(rank))
         for r in range(world):

@@ -65,22 +65,47 @@ __device__ __forceinline__ u64 block_sum(u64 v, u64* lds4) {
 
 // ---------------------------------------------------------------------------
 // k_copy: dst[0:n) = src[0:n).  n16 = n / 16 vector units; the tail bytes are
-// copied by block 0.  Grid-stride with U independent 16-B loads per lane in
-// flight; nontemporal (streaming) loads and stores: every byte is touched once.
+// copied by block 0.  Every lane keeps U independent 16-B loads in flight.
+//   CONTIG = false: grid-stride over the whole buffer (unit i, i+G, ...)
+//   CONTIG = true : block b owns one contiguous chunk, swept 4 KiB per step
+//   LDNT / STNT   : nontemporal (streaming) loads / stores
+// The variant is chosen at launch (launch_copy; MPX_COPY_VARIANT overrides
+// for tuning sweeps).
 // ---------------------------------------------------------------------------
-template <int U>
+template <bool NT>
+__device__ __forceinline__ v4u ld16(const v4u* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(v4u* p, v4u v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int U, bool LDNT, bool STNT, bool CONTIG>
 __global__ __launch_bounds__(kBlock) void k_copy(const v4u* __restrict__ src, v4u* __restrict__ dst,
                                                 size_t n16, unsigned tail) {
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + (U - 1) * stride < n16; i += U * stride) {
+    size_t i, end, stride;
+    if constexpr (CONTIG) {
+        const size_t per = (n16 + gridDim.x - 1) / gridDim.x;
+        const size_t lo = (size_t)blockIdx.x * per;
+        end = lo + per < n16 ? lo + per : n16;
+        i = lo + threadIdx.x;
+        stride = kBlock;
+    } else {
+        end = n16;
+        i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+        stride = (size_t)gridDim.x * kBlock;
+    }
+    for (; i + (U - 1) * stride < end; i += U * stride) {
         v4u r[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = __builtin_nontemporal_load(src + i + u * stride);
+        for (int u = 0; u < U; ++u) r[u] = ld16<LDNT>(src + i + u * stride);
 #pragma unroll
-        for (int u = 0; u < U; ++u) __builtin_nontemporal_store(r[u], dst + i + u * stride);
+        for (int u = 0; u < U; ++u) st16<STNT>(dst + i + u * stride, r[u]);
     }
-    for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    for (; i < end; i += stride) st16<STNT>(dst + i, ld16<LDNT>(src + i));
     if (blockIdx.x == 0 && threadIdx.x < tail) {
         const unsigned char* s8 = reinterpret_cast<const unsigned char*>(src + n16);
         unsigned char* d8 = reinterpret_cast<unsigned char*>(dst + n16);
@@ -423,15 +448,54 @@ hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
+typedef void (*copy_fn)(const v4u*, v4u*, size_t, unsigned);
+
+#define COPY_VARIANTS(U)                                                                            \
+    {U, 0, 0, 0, k_copy<U, false, false, false>}, {U, 1, 0, 0, k_copy<U, true, false, false>},     \
+    {U, 0, 1, 0, k_copy<U, false, true, false>},  {U, 1, 1, 0, k_copy<U, true, true, false>},      \
+    {U, 0, 0, 1, k_copy<U, false, false, true>},  {U, 1, 0, 1, k_copy<U, true, false, true>},      \
+    {U, 0, 1, 1, k_copy<U, false, true, true>},   {U, 1, 1, 1, k_copy<U, true, true, true>}
+
+struct CopyVariant {
+    int u, ldnt, stnt, contig;
+    copy_fn fn;
+};
+static const CopyVariant kCopyVariants[] = {COPY_VARIANTS(2), COPY_VARIANTS(4), COPY_VARIANTS(8), COPY_VARIANTS(16)};
+
+// Default from the tuning sweeps (DESIGN.md "k_copy tuning", profiles/
+// copy_sweep_r01.jsonl): 2 loads in flight per lane, nontemporal loads and
+// stores, one contiguous 8-16 KiB chunk per block, up to 256 blocks per CU.
+// 1 GiB: 6.2-6.4 TB/s of HBM traffic (grid-stride, 16 blocks/CU: 4.5 TB/s).
+struct CopyConfig {
+    int u = 2, ldnt = 1, stnt = 1, contig = 1, blocks_per_cu = 256;
+};
+
+static CopyConfig copy_config() {
+    CopyConfig c;
+    // MPX_COPY_VARIANT="U:ldnt:stnt:contig:blocks_per_cu"
+    if (const char* v = getenv("MPX_COPY_VARIANT")) {
+        int a[5];
+        if (sscanf(v, "%d:%d:%d:%d:%d", &a[0], &a[1], &a[2], &a[3], &a[4]) == 5) {
+            c.u = a[0]; c.ldnt = a[1]; c.stnt = a[2]; c.contig = a[3]; c.blocks_per_cu = a[4];
+        }
+    }
+    return c;
+}
+
 hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int* grid_out) {
+    static const CopyConfig cfg = copy_config();
+    copy_fn fn = nullptr;
+    for (const CopyVariant& v : kCopyVariants)
+        if (v.u == cfg.u && v.ldnt == cfg.ldnt && v.stnt == cfg.stnt && v.contig == cfg.contig) fn = v.fn;
+    if (!fn) return hipErrorInvalidValue;
     const size_t n16 = n / 16;
     const unsigned tail = (unsigned)(n & 15);
-    constexpr int U = 4;
-    size_t grid = (n16 + (size_t)kBlock * U - 1) / ((size_t)kBlock * U);
-    if (grid > 4096) grid = 4096;     // 16 blocks per CU, grid-stride beyond
+    size_t grid = (n16 + (size_t)kBlock * cfg.u - 1) / ((size_t)kBlock * cfg.u);
+    const size_t cap = (size_t)256 * (cfg.blocks_per_cu > 0 ? cfg.blocks_per_cu : 16);
+    if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
     if (grid_out) *grid_out = (int)grid;
-    hipLaunchKernelGGL(k_copy<U>, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const v4u*>(src),
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const v4u*>(src),
                        reinterpret_cast<v4u*>(dst), n16, tail);
     return hipGetLastError();
 }

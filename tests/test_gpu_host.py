@@ -1,0 +1,95 @@
+"""The mpx_perf executable on the GPU (two or four ranks sharing GPU 0):
+records, log files and check mode, compared with the reference's golden
+runs (same flags) and the record format."""
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PERF = os.path.join(ROOT, "mpi-perf_amd", "bin", "mpx_perf")
+GOLDEN = {c["name"]: c for c in O.golden()["cases"]}
+
+
+def run(tmp_path, args, lines=("vm",), names="vm,runsc", gpus="0,0"):
+    g1 = tmp_path / "group1"
+    g1.write_text("".join(x + "\n" for x in lines))
+    logs = tmp_path / "logs"
+    argv = [a.replace("@G1", str(g1)).replace("@LOGS", str(logs)) for a in args]
+    env = dict(os.environ, MPX_PROCESSOR_NAMES=names)
+    p = subprocess.run([PERF, "-g", gpus, "-t", "5000"] + argv, capture_output=True, text=True, env=env, timeout=120)
+    recs = []
+    for f in sorted(glob.glob(str(logs / "tcp-*.log"))):
+        recs += [line.rstrip("\n").split(",") for line in open(f)]
+    side = []
+    for f in sorted(glob.glob(str(logs / "gpu-*.csv"))):
+        side += [line.rstrip("\n").split(",") for line in open(f)][1:]
+    return p, recs, side
+
+
+@pytest.mark.parametrize("name", ["pingpong_p1_b456131_i3", "unidir_p2_b4096_i7", "nonblocking_p2_b8_i10",
+                                  "unidir_p1_b8_i10", "pingpong_p2_b1_i10"])
+def test_records_match_reference_run(tmp_path, name):
+    c = GOLDEN[name]
+    names = ",".join(["vm"] * c["ppn"] + ["runsc"] * c["ppn"])
+    gpus = ",".join(["0"] * c["np"])
+    p, recs, side = run(tmp_path, ["-w", str(c["np"])] + c["args"] + ["-c", "1"], names=names, gpus=gpus)
+    assert p.returncode == 0, p.stderr[-600:]
+    assert len(recs) == c["n_records"]
+    ref = sorted((r["rank"], r["vmcount"], r["flows"], r["buffer_size"], r["num_buffers"], r["run_id"])
+                 for r in c["records"])
+    mine = sorted((int(f[2]), int(f[3]), int(f[6]), int(f[7]), int(f[8]), int(f[10])) for f in recs)
+    assert mine[:len(ref)] == ref
+    for f in recs:
+        assert len(f) == 11 and re.fullmatch(r"\d{4}-\d\d-\d\d \d\d:\d\d:\d\d", f[0])
+        assert re.fullmatch(r"\d+\.\d\d", f[9])
+    # INFO lines carry the same pairing as the reference's
+    info = re.findall(r"INFO: (\S+), rank (\d+) out of (\d+) ranks, my_group: (\d), group_size: (\d+), "
+                      r"group_rank: (\d+), my_peer: (-?\d+)", p.stderr)
+    assert sorted((int(x[1]), int(x[3]), int(x[4]), int(x[5]), int(x[6])) for x in info) == \
+        sorted((d["rank"], d["group"], d["group_size"], d["group_rank"], d["peer"]) for d in c["info"])
+    # every checked payload passed
+    for f in side:
+        if f[4] != "1":       # nonblocking: final rx only
+            assert int(f[16]) == 0 and int(f[15]) == int(f[9])
+
+
+def test_seeded_pattern_check_and_sweep(tmp_path):
+    p, recs, side = run(tmp_path, ["-w", "2", "-f", "@G1", "-n", "1", "-p", "1", "-r", "3", "-i", "5", "-S",
+                                   "1:1048576", "-c", "2", "-l", "@LOGS"])
+    assert p.returncode == 0, p.stderr[-600:]
+    sizes = sorted({int(f[7]) for f in recs})
+    assert sizes == [1 << k for k in range(21)]
+    assert len(recs) == 21 * 2
+
+
+def test_all_pairs_rounds_on_one_gpu(tmp_path):
+    p, recs, side = run(tmp_path, ["-w", "4", "-a", "1", "-f", "@G1", "-n", "1", "-p", "2", "-u", "1", "-r", "7",
+                                   "-i", "4", "-b", "65536", "-c", "1", "-l", "@LOGS"], names="vm,vm,runsc,runsc",
+                        gpus="0,0,0,0")
+    assert p.returncode == 0, p.stderr[-600:]
+    rounds = re.findall(r"ROUND (\d+): (.*)", p.stderr)
+    assert len(rounds) == 3
+    # 6 of 7 runs are recorded, 2 senders each
+    assert len(recs) == 6 * 2
+    pairs = {(int(f[2]), int(f[6])) for f in side}
+    assert len(pairs) >= 3
+
+
+def test_engines_sdma(tmp_path):
+    p, recs, side = run(tmp_path, ["-w", "2", "-e", "sdma", "-f", "@G1", "-n", "1", "-p", "1", "-r", "3", "-i", "20",
+                                   "-b", "1048576", "-c", "1", "-l", "@LOGS"])
+    assert p.returncode == 0, p.stderr[-600:]
+    assert len(recs) == 2 and all(f[13] == "sdma" for f in side)
+
+
+def test_unidir_without_ppn_raises_sigfpe_like_reference(tmp_path):
+    c = GOLDEN["err_unidir_no_ppn_sigfpe"]
+    p, recs, side = run(tmp_path, ["-w", "2"] + c["args"])
+    assert p.returncode == -8 and c["returncode"] == 8
+    assert len(re.findall(r"INFO: ", p.stderr)) == len(c["info"])

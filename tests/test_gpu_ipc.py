@@ -1,0 +1,34 @@
+"""Two PROCESSES on GPU 0 exchange payloads through libmpx's IPC path
+(mpx_rank_export / mpx_rank_import), the path bench.py uses for one process
+per GPU.  Every payload is checksummed; the final rx must equal the peer's tx.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+def test_two_process_ipc_pair(tmp_path, engine):
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "ipc_worker.py"), str(tmp_path), str(r), engine],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in (0, 1)]
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=100)[0])
+        except subprocess.TimeoutExpired:
+            p.kill()
+            outs.append(p.communicate()[0])
+    assert all(p.returncode == 0 for p in procs), outs
+    for r in (0, 1):
+        res = json.load(open(tmp_path / f"result_{r}.json"))
+        assert len(res) == 15
+        for x in res:
+            assert x["final_rx_ok"], (r, x)
+            if x["mode"] != 1:
+                assert x["check_failures"] == 0 and x["check_iters"] == 9, (r, x)
