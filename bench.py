@@ -123,6 +123,103 @@ def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: in
         return dict(median_s=statistics.median(res[1:]), per_iter_us=statistics.median(res[1:]) / iters * 1e6)
 
 
+def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
+                latency=True) -> dict:
+    """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers).
+    Every round's payloads are validated once (check mode, seeded per-rank
+    patterns) before anything is timed.  Returns a dict; "error" is set (on
+    every rank) if any rank failed."""
+    from mpx.schedule import all_pairs_rounds, round_role
+
+    rounds = all_pairs_rounds(world)
+    out = {}
+    c = None
+
+    def agree(err: str) -> str:
+        """every rank learns the first error of any rank (one gloo collective)"""
+        flags = [None] * world
+        dist.all_gather_object(flags, err)
+        return next((f for f in flags if f), "")
+
+    # phase 1: local setup (no collectives inside the try)
+    mine, err = None, ""
+    try:
+        c = mpx.Context(world, engine)
+        tx, rx = c.alloc(dev, nbytes), c.alloc(dev, nbytes)
+        c.fill(tx, nbytes, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, rank, 0, 0))
+        c.attach(rank, dev, tx, rx, nbytes)
+        mine = (c.export(rank), c.checksum(tx, nbytes), c.checksum(tx, 1))
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
+    descs = [None] * world
+    dist.all_gather_object(descs, mine)
+    err = agree(err)
+    uid = [None]
+    if engine == "rccl" and not err:
+        uid = [mpx.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+    # phase 2: map the peers, validate every round once (collectives only
+    # between the phases: each pair synchronises itself inside xfer)
+    if not err:
+        try:
+            for r in range(world):
+                if r != rank:
+                    c.import_rank(r, descs[r][0])
+            if engine == "rccl":
+                c.rccl_init_rank(rank, world, uid[0])
+            for r in range(len(rounds)):
+                g, peer = round_role(rounds, r, rank)
+                c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True,
+                       expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000)
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
+        err = agree(err)
+    if err:
+        if c is not None:
+            try:
+                c.close()
+            except Exception:  # noqa: BLE001
+                pass
+        return {"error": err}
+    out["validated_rounds"] = len(rounds)
+
+    def step(s: int):
+        g, peer = round_role(rounds, s % len(rounds), rank)
+        dist.barrier()                               # MPI_Barrier, mpi_perf.c:499
+        return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes)
+
+    for s in range(warmup):
+        step(s)
+    dev_s, n_sends = 0.0, 0
+    barrier_sync()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        g, t = step(s)
+        if g == 1:
+            dev_s += t.device_s
+            n_sends += 1
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    tt = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    out["elapsed"] = float(tt[0])
+    out["total"] = (world // 2) * nbytes * iters * steps
+    st = torch.tensor([dev_s, float(n_sends)], dtype=torch.float64)
+    dist.all_reduce(st, op=dist.ReduceOp.SUM)
+    out["per_launch_s"] = float(st[0]) / max(float(st[1]), 1.0)
+    out["per_pair_GBps"] = nbytes * iters / out["per_launch_s"] / 1e9
+    if latency:
+        g, peer = round_role(rounds, 0, rank)
+        dist.barrier()
+        lt = c.xfer(mpx.MODE_PINGPONG, g, rank, peer, 2000, tx, rx, 8)
+        lat = torch.tensor([lt.wall_s], dtype=torch.float64)
+        dist.all_reduce(lat, op=dist.ReduceOp.MAX)
+        out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / 4000 * 1e6, 3)
+    dist.barrier()
+    c.close()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,8 +256,11 @@ def main() -> None:
     torch.cuda.set_device(dev)
     dist = None
     if not one:
+        import datetime
+
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # a rank that dies must not leave the others in a 30-minute gloo wait
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=180))
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -208,64 +308,39 @@ def main() -> None:
             extras["loopback_unidir_4MiB_GBps"] = round((4 << 20) / (uni["per_iter_us"] * 1e-6) / 1e9, 2)
         c.close()
     else:
-        from mpx.schedule import all_pairs_rounds, round_role
         workload = "all_pairs_rounds_unidir"
-        c = mpx.Context(world, args.engine)
-        tx, rx = c.alloc(dev, nbytes), c.alloc(dev, nbytes)
-        c.fill(tx, nbytes, mpx.FILL_BYTE, ord("b"))
-        c.attach(rank, dev, tx, rx, nbytes)
-        descs = [None] * world
-        dist.all_gather_object(descs, c.export(rank))
-        for r in range(world):
-            if r != rank:
-                c.import_rank(r, descs[r])
-        if args.engine == "rccl":
-            uid = [mpx.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            c.rccl_init_rank(rank, world, uid[0])
-        rounds = all_pairs_rounds(world)
-
-        def step(s: int):
-            g, peer = round_role(rounds, s % len(rounds), rank)
-            dist.barrier()                           # MPI_Barrier, mpi_perf.c:499
-            return c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes)
-
-        for s in range(args.warmup):
-            step(s)
-        dev_s, n_sends = 0.0, 0
-        barrier_sync()
-        t0 = time.perf_counter()
-        for s in range(args.steps):
-            t = step(s)
-            if round_role(rounds, s % len(rounds), rank)[0] == 1:
-                dev_s += t.device_s
-                n_sends += 1
-        barrier_sync()
-        elapsed = time.perf_counter() - t0
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt[0])
-        total = (world // 2) * nbytes * iters * args.steps
-        st = torch.tensor([dev_s, float(n_sends)], dtype=torch.float64)
-        dist.all_reduce(st, op=dist.ReduceOp.SUM)
-        per_launch = float(st[0]) / max(float(st[1]), 1.0)
-        algo = nbytes * iters   # bytes one k_xfer launch pushes over its link
-        achieved = algo / per_launch / 1e9
-        roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",
-                    frac=round(achieved / XGMI_LINK_PEAK_GBPS, 4), traffic=None, kernel="k_xfer (G1 side)",
-                    avg_launch_us=round(per_launch * 1e6, 2), algorithmic_bytes_per_launch=algo)
-        config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=args.engine,
-                      rounds=len(rounds), pairs_per_round=world // 2, parallelism=f"pairs{world // 2}")
         metric_unit = "GB/s"
+        res = pairs_bench(mpx, torch, dist, args.engine, rank, world, dev, nbytes, iters, args.steps, args.warmup,
+                          barrier_sync)
+        engine_used = args.engine
+        if res.get("error") and args.engine == "kernel":
+            # explicit, labelled fallback: the kernel engine failed payload
+            # validation or timed out on this node; measure the SDMA engine
+            fb = pairs_bench(mpx, torch, dist, "sdma", rank, world, dev, nbytes, iters, args.steps, args.warmup,
+                             barrier_sync)
+            extras["kernel_engine_error"] = res["error"]
+            res, engine_used = fb, "sdma (fallback: kernel engine failed validation)"
+        if res.get("error"):
+            raise SystemExit(f"pairs bench failed: {res['error']}")
+        elapsed, total = res["elapsed"], res["total"]
+        achieved = res["per_pair_GBps"]
+        roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",
+                    frac=round(achieved / XGMI_LINK_PEAK_GBPS, 4), traffic=None,
+                    kernel="k_xfer (G1 side)" if engine_used == "kernel" else engine_used,
+                    avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
+        config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=engine_used,
+                      rounds=world - 1, pairs_per_round=world // 2, parallelism=f"pairs{world // 2}",
+                      validated_rounds=res["validated_rounds"])
+        extras["per_pair_unidir_GBps"] = round(achieved, 2)
+        if "pingpong_8B_half_rtt_us" in res:
+            extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
         if not args.no_extras:
-            g, peer = round_role(rounds, 0, rank)
-            dist.barrier()
-            lt = c.xfer(mpx.MODE_PINGPONG, g, rank, peer, 2000, tx, rx, 8)
-            lat = torch.tensor([lt.wall_s], dtype=torch.float64)
-            dist.all_reduce(lat, op=dist.ReduceOp.MAX)
-            extras["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / 4000 * 1e6, 3)
-            extras["per_pair_unidir_GBps"] = round(achieved, 2)
-        c.close()
+            for eng in ("sdma", "rccl"):
+                if eng == engine_used:
+                    continue
+                r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, max(10, iters // 5),
+                                 world - 1, 1, barrier_sync, latency=False)
+                extras[f"{eng}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
 
     value = total / elapsed / 1e9
     if rank == 0:

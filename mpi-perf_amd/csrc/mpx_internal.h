@@ -62,7 +62,17 @@ struct XferArgs {
     int peer_slot;               // peer rank = its slot in my mailbox
     int nwg;                     // bulk push workgroups (same on both sides)
     int check;                   // 1 = checksum + poison each received payload
+    int ll_flags;                // bit0: 16-B stores (2 granules each), else 8-B;
+                                 // bit1: poll one sentinel granule first, then sweep
+    int ll_max;                  // messages <= ll_max bytes use LL (<= kLLMaxBytes);
+                                 // same on both sides of the link
 };
+
+// LL threshold of a link.  Within one GPU the bulk path's extra hop (payload
+// drain, then flag) is cheap and bulk wins above ~2 KiB (loopback sweep,
+// profiles/r01_loopback_sweep.jsonl); across xGMI that hop is a full link
+// round trip, so LL is kept up to its 8 KiB landing zone.
+inline int ll_max_bytes(bool same_device) { return same_device ? 2048 : kLLMaxBytes; }
 
 // LL granule tag for push sequence number `seq` (>= 1): never 0, so a zeroed
 // mailbox can never match, and distinct for seqs < 2^31 apart.

@@ -207,24 +207,39 @@ struct Loop {
         return now_ticks() - t0 > a.timeout_ticks;
     }
 
-    __device__ bool is_ll(long long n) const { return a.mode != MPX_MODE_NONBLOCKING && n <= kLLMaxBytes; }
+    __device__ bool is_ll(long long n) const { return a.mode != MPX_MODE_NONBLOCKING && n <= a.ll_max; }
 
     // ---- send: push n bytes of tx[0:n) into the peer's rx -------------------
+    // LL: one workgroup; every 16-B store carries two granules {payload:32,
+    // tag:32} (each 8-B half lands untorn), so 8 payload bytes per store.
     __device__ void push_ll(long long n, u64 seq) const {
         if (blockIdx.x != 0) return;
         const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;   // a 0-byte message is one empty granule
-        const u64 tag = (u64)ll_tag(seq) << 32;
-        u64* g = &a.peer_mb->ll[a.my_slot][0];
-        for (int k = threadIdx.x; k < ng; k += kBlock) {
-            unsigned d;
-            const long long off = 4ll * k;
-            if (off + 4 <= n) {
-                d = *reinterpret_cast<const unsigned*>(a.tx + off);
-            } else {
-                d = 0;
-                for (long long b = 0; off + b < n; ++b) d |= (unsigned)a.tx[off + b] << (8 * b);
+        const int nu = (ng + 1) >> 1;                      // 16-B units
+        const unsigned tag = ll_tag(seq);
+        if (!(a.ll_flags & 1)) {   // one 8-B system-scope store per granule
+            u64* g = &a.peer_mb->ll[a.my_slot][0];
+            for (int k = threadIdx.x; k < ng; k += kBlock) {
+                const long long off = 4ll * k;
+                unsigned d = 0;
+                if (off + 4 <= n) d = *reinterpret_cast<const unsigned*>(a.tx + off);
+                else for (long long b = 0; off + b < n; ++b) d |= (unsigned)a.tx[off + b] << (8 * b);
+                st_sys(g + k, ((u64)tag << 32) | d);
             }
-            st_sys(g + k, tag | d);
+            return;
+        }
+        const __amdgpu_buffer_rsrc_t dst = rsrc(&a.peer_mb->ll[a.my_slot][0], (unsigned)(nu * 16));
+        for (int u = threadIdx.x; u < nu; u += kBlock) {
+            const long long off = 8ll * u;
+            u64 w;
+            if (off + 8 <= n) {
+                w = *reinterpret_cast<const u64*>(a.tx + off);
+            } else {
+                w = 0;
+                for (long long b = 0; off + b < n; ++b) w |= (u64)a.tx[off + b] << (8 * b);
+            }
+            const v4u v = {(unsigned)w, tag, (unsigned)(w >> 32), tag};
+            __builtin_amdgcn_raw_buffer_store_b128(v, dst, (unsigned)u * 16, 0, kAuxSys);
         }
     }
 
@@ -264,27 +279,57 @@ struct Loop {
     }
 
     // ---- receive: wait until the peer's push `seq` of n bytes has landed ----
+    // LL receive: every lane issues the loads of ALL its granules (up to 8)
+    // back to back, then checks the tags — one memory round trip per poll,
+    // not one per granule.
     __device__ bool wait_ll(long long n, u64 seq, int iter) const {
+        constexpr int kPer = kLLGranules / kBlock;         // granules per lane, max
         const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;
+        const int mine = ng > (int)threadIdx.x ? (ng - (int)threadIdx.x + kBlock - 1) / kBlock : 0;
         const unsigned tag = ll_tag(seq);
-        const u64* g = &a.my_mb->ll[a.peer_slot][0];
-        const bool unpack = blockIdx.x == 0;
-        // a multi-granule LL message is only ever received by a 1-WG grid
-        for (int k = threadIdx.x; k < ng; k += kBlock) {
+        const u64* g = &a.my_mb->ll[a.peer_slot][threadIdx.x];
+        u64 x[kPer];
+        if ((a.ll_flags & 2) && ng > 2) {
+            // sentinel: one lane polls the message's last granule before the
+            // whole workgroup sweeps (less polling traffic on the landing zone)
+            if (threadIdx.x == 0) {
+                const u64* last = &a.my_mb->ll[a.peer_slot][ng - 1];
+                const u64 t0 = now_ticks();
+                u64 spins = 0;
+                while ((unsigned)(ld_sys(last) >> 32) != tag) {
+                    if (should_stop(++spins, t0)) { give_up(iter); break; }
+                    __builtin_amdgcn_s_sleep(0);
+                }
+            }
+            __syncthreads();
+            if (aborted()) return false;
+        }
+        if (mine > 0) {
             const u64 t0 = now_ticks();
-            u64 x, spins = 0;
-            while ((unsigned)((x = ld_sys(g + k)) >> 32) != tag) {
+            u64 spins = 0;
+            for (;;) {
+#pragma unroll
+                for (int j = 0; j < kPer; ++j)
+                    if (j < mine) x[j] = ld_sys(g + j * kBlock);
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < kPer; ++j)
+                    if (j < mine) ok &= (unsigned)(x[j] >> 32) == tag;
+                if (ok) break;
                 if (should_stop(++spins, t0)) { give_up(iter); break; }
                 __builtin_amdgcn_s_sleep(0);
             }
-            if (*s_abort) break;
-            if (unpack) {
-                const long long off = 4ll * k;
-                const unsigned d = (unsigned)x;
-                if (off + 4 <= n) {
-                    *reinterpret_cast<unsigned*>(a.rx + off) = d;
-                } else {
-                    for (long long b = 0; off + b < n; ++b) a.rx[off + b] = (unsigned char)(d >> (8 * b));
+            if (blockIdx.x == 0 && !*s_abort) {
+#pragma unroll
+                for (int j = 0; j < kPer; ++j) {
+                    if (j >= mine) break;
+                    const long long off = 4ll * ((int)threadIdx.x + j * kBlock);
+                    const unsigned d = (unsigned)x[j];
+                    if (off + 4 <= n) {
+                        *reinterpret_cast<unsigned*>(a.rx + off) = d;
+                    } else {
+                        for (long long b = 0; off + b < n; ++b) a.rx[off + b] = (unsigned char)(d >> (8 * b));
+                    }
                 }
             }
         }

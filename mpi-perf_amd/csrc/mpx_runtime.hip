@@ -284,6 +284,15 @@ bool same_device(const Rank& a, const Rank& b) {
     return a.bus_id[0] && strcmp(a.bus_id, b.bus_id) == 0;
 }
 
+// LL protocol knobs (DESIGN.md "LL"): MPX_LL_FLAGS overrides for sweeps.
+int ll_flags() {
+    static const int f = [] {
+        const char* v = getenv("MPX_LL_FLAGS");
+        return v ? atoi(v) : 1;   // default: 16-B stores, all lanes poll (LL A/B)
+    }();
+    return f;
+}
+
 u64 timeout_ticks(const mpx_xfer_opts* o) {
     const u64 ms = (o && o->timeout_ms) ? o->timeout_ms : 10000;
     return ms * 100000ull;   // s_memrealtime runs at 100 MHz
@@ -316,8 +325,11 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.nwg = (o && o->nwg > 0) ? o->nwg : bulk_nwg(len, same_device(me, peer));
     if (a.nwg > kMaxPushWG) return fail(MPX_ERR_INVALID, "nwg %d > %d", a.nwg, kMaxPushWG);
     a.check = (o && o->check) ? 1 : 0;
+    a.ll_flags = ll_flags();
+    a.ll_max = ll_max_bytes(same_device(me, peer));
+    if (const char* v = getenv("MPX_LL_MAX")) a.ll_max = atoi(v) < kLLMaxBytes ? atoi(v) : kLLMaxBytes;
 
-    const bool ll = mode != MPX_MODE_NONBLOCKING && len <= kLLMaxBytes;
+    const bool ll = mode != MPX_MODE_NONBLOCKING && len <= a.ll_max;
     const bool pushes_len = mode != MPX_MODE_UNIDIR || group == 1;
     const bool recvs_len = mode != MPX_MODE_UNIDIR || group == 0;
     const int grid = (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;

@@ -251,3 +251,23 @@ def test_invalid_arguments(ctx):
             ctx.xfer(0, 1, 0, 1, 1, b, b, 8)          # rank 0 not attached
     finally:
         ctx.free(b)
+
+
+@pytest.mark.parametrize("mode", [mpx.MODE_PINGPONG, mpx.MODE_UNIDIR])
+def test_ll_full_landing_zone(monkeypatch, mode):
+    """Cross-GPU links use LL up to 8 KiB (ll_max_bytes); loopback links switch
+    at 2 KiB.  Force the cross-GPU threshold to cover the whole landing zone."""
+    monkeypatch.setenv("MPX_LL_MAX", "8192")
+    P = Pairs("kernel", 1, 8192 + 64)
+    try:
+        for n in (2049, 4095, 4096, 8191, 8192):
+            out, errs = P.run(mode, n, 11)
+            assert not errs, (n, errs)
+            for r in (0, 1):
+                assert out[r].check_failures == 0 and out[r].check_iters == 11
+            assert out[0].protocol == PROTO_LL
+    finally:
+        P.close()
+
+
+PROTO_LL = 0
