@@ -63,6 +63,8 @@ static uint64_t txsum_of[MPXH_MAX_RANKS], txsum1_of[MPXH_MAX_RANKS];
 static pthread_barrier_t bar;
 static int report_bandwidth;
 static int sizes[40], nsizes;
+/* LOG_REFRESH_TIME_SEC (mpi_perf.c:16); MPX_LOG_REFRESH_SEC overrides it for tests */
+static double log_refresh_sec = MPXH_LOG_REFRESH_SEC;
 
 static double wtime(void) /* MPI_Wtime */
 {
@@ -142,8 +144,7 @@ static void *rank_main(void *arg)
                     prev_group = group;
                 }
             }
-            if (group == 1 &&
-                (files.log_fp == NULL || (wtime() - files.t_last_logtime) > MPXH_LOG_REFRESH_SEC))
+            if (group == 1 && (files.log_fp == NULL || (wtime() - files.t_last_logtime) > log_refresh_sec))
                 open_logs(r, &files);
 
             mpx_xfer_opts xo;
@@ -237,6 +238,7 @@ int main(int argc, char **argv)
     report_bandwidth = getenv("MPX_REPORT_BANDWIDTH") != NULL;
 #endif
 
+    if (getenv("MPX_LOG_REFRESH_SEC")) log_refresh_sec = atof(getenv("MPX_LOG_REFRESH_SEC"));
     world = opt.world > 0 ? opt.world : (opt.ppn > 0 ? 2 * opt.ppn : 2);
     if (world > MPXH_MAX_RANKS || world > MPX_MAX_RANKS) {
         fprintf(stderr, "at most %d ranks\n", MPXH_MAX_RANKS);
@@ -277,8 +279,10 @@ int main(int argc, char **argv)
         }
     }
 
-    int ndev = 0;
-    MPX_CHECK(mpx_device_count(&ndev));
+    /* the .NET mode only prints launcher lines (mpi_perf.c:147-168) and, like
+       the reference, allocates nothing: it needs no GPU */
+    int ndev = world;
+    if (!opt.use_dotnet) MPX_CHECK(mpx_device_count(&ndev));
     if (opt.gpus[0]) {
         if (mpxh_parse_gpu_list(opt.gpus, dev_of, MPXH_MAX_RANKS) < world) {
             fprintf(stderr, "-g lists fewer GPUs than ranks (%d)\n", world);
@@ -323,7 +327,7 @@ int main(int argc, char **argv)
         if (sizes[i] > maxb) maxb = sizes[i];
 
     if (opt.logfolder[0]) mkdir(opt.logfolder, 0755);
-    MPX_CHECK(mpx_init(world, opt.engine, &ctx));
+    if (!opt.use_dotnet) MPX_CHECK(mpx_init(world, opt.engine, &ctx));
     if (!opt.use_dotnet) { /* allocate_tx_rx_buffers, mpi_perf.c:463-468 */
         for (int r = 0; r < world; ++r) {
             MPX_CHECK(mpx_alloc(ctx, dev_of[r], (size_t)maxb, &tx_of[r]));
@@ -346,6 +350,6 @@ int main(int argc, char **argv)
             MPX_CHECK(mpx_free(ctx, rx_of[r]));
         }
     }
-    MPX_CHECK(mpx_finalize(ctx));
+    if (ctx) MPX_CHECK(mpx_finalize(ctx));
     return 0;
 }

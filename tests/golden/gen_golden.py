@@ -87,6 +87,7 @@ def run_case(name, np_, ppn, args, group1_lines=("vm",), host1="vm", host0="runs
             d = json.load(open(path))
             shim[str(d["rank"])] = {k: d[k] for k in ("recv_done", "recv_bytes", "recv_digest", "waitall_calls",
                                                       "waitall_reqs")}
+        dotnet = sorted(re.findall(r"^dotnet .*$", err, flags=re.M))
         messages = []
         for key in ("invalid group_size", "getaddrinfo error", "Usage: <program>", "cannot open group1 file",
                     "failed to read OMPI_COMM_WORLD_LOCAL_RANK"):
@@ -94,7 +95,7 @@ def run_case(name, np_, ppn, args, group1_lines=("vm",), host1="vm", host0="runs
                 messages.append(key)
         return dict(name=name, np=np_, ppn=ppn, args=args, group1_lines=list(group1_lines), host1=host1, host0=host0,
                     returncode=p.returncode, uuid_printed=bool(re.search(r"UUID: " + UUID_RE.pattern, err)),
-                    info=info, summaries=summaries, files=files, records=records, n_records=n_records, shim=shim, messages=messages)
+                    info=info, summaries=summaries, files=files, records=records, n_records=n_records, shim=shim, messages=messages, dotnet=dotnet)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -131,6 +132,16 @@ def main():
     # --- summary printed by rank 0 every 1000 runs (mpi_perf.c:564) ---
     cases.append(run_case("summary_every_1000", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-r", "1002", "-i", "1",
                                                        "-b", "1", "-l", "@LOGS"]))
+    # --- flag interplay and degenerate loops ---
+    cases.append(run_case("unidir_wins_over_nonblocking", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-u", "1", "-x",
+                                                                 "1", "-r", "2", "-i", "4", "-b", "16", "-l", "@LOGS"]))
+    cases.append(run_case("zero_runs", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-r", "0", "-i", "4", "-b", "16",
+                                              "-l", "@LOGS"]))
+    cases.append(run_case("zero_iters", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-r", "3", "-i", "0", "-b", "16",
+                                               "-l", "@LOGS"]))
+    # --- the .NET launcher mode only prints its command lines (mpi_perf.c:147-168) ---
+    cases.append(run_case("dotnet_print_only", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-d", "1", "-r", "2", "-i",
+                                                      "7", "-b", "64", "-l", "@LOGS"]))
     # --- error exits ---
     cases.append(run_case("err_bidir_no_ppn_sigfpe", 2, 1, ["-f", "@G1", "-n", "1", "-r", "2", "-i", "3", "-b", "8",
                                                            "-l", "@LOGS"]))

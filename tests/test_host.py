@@ -164,3 +164,40 @@ def test_cli_error_exits_match_reference(tmp_path, name):
     for msg in c["messages"]:
         assert msg in p.stderr, (msg, p.stderr[-400:])
     assert ("UUID: " in p.stderr) == c["uuid_printed"] or name in ("err_unknown_flag", "err_h_flag")
+
+
+def _mask_ip(line):
+    return re.sub(r"\d+\.\d+\.\d+\.\d+(:gpu\d+)?", "IP", line)
+
+
+def test_dotnet_mode_matches_reference(tmp_path):
+    """-d 1 prints the launcher command per rank per run and writes no record
+    (mpi_perf.c:147-168, :545); it needs no GPU, like the reference."""
+    c = CASES["dotnet_print_only"]
+    p = run_perf(["-w", "2"] + c["args"], tmp_path, lines=c["group1_lines"], names="vm,runsc")
+    assert p.returncode == 0, p.stderr[-500:]
+    mine = sorted(_mask_ip(x) for x in re.findall(r"^dotnet .*$", p.stderr, flags=re.M))
+    assert mine == sorted(_mask_ip(x) for x in c["dotnet"])
+    logs = tmp_path / "logs"
+    assert len(list(logs.glob("tcp-*.log"))) == len(c["files"]) == 1
+    assert all(f.stat().st_size == 0 for f in logs.glob("tcp-*.log")) and c["n_records"] == 0
+    assert ("[Run#: 0]" in p.stderr) == (c["summaries"] == [0])
+
+
+def test_kusto_file_selection_contract(tmp_path):
+    """kusto_ingest.py:32-40 ingests files in the log dir whose name starts with
+    'tcp' (case-insensitive), all but the newest n by mtime.  The GPU side
+    files must never be selected."""
+    import time
+    logs = tmp_path / "logs"
+    logs.mkdir()
+    names = ["tcp-u-0-2026-01-01-00-00-00.log", "tcp-u-0-2026-01-01-00-15-00.log", "gpu-u-0-x.csv",
+             "TCP-u-1-2026-01-01-00-00-00.log"]
+    for i, n in enumerate(names):
+        (logs / n).write_text("x\n")
+        os.utime(logs / n, (1000 + i, 1000 + i))
+    files = [f for f in os.listdir(logs) if (logs / f).is_file() and f.lower().startswith("tcp")]
+    files.sort(key=lambda f: os.path.getmtime(logs / f))
+    picked = files[:-1]
+    assert "gpu-u-0-x.csv" not in files and len(picked) == 2
+    del time

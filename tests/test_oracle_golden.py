@@ -123,9 +123,12 @@ def test_records_and_files_per_sender(name):
     c = CASES[name]
     runs = _arg(c, "-r", 1)
     senders = [d["rank"] for d in c["info"] if d["group"] == 1]
-    assert c["n_records"] == len(senders) * max(0, runs - 1)
+    dotnet = "-d" in c["args"] and c["args"][c["args"].index("-d") + 1] == "1"
+    # records: senders only, runs 1.. only, never in .NET mode (mpi_perf.c:545)
+    assert c["n_records"] == (0 if dotnet else len(senders) * max(0, runs - 1))
     assert all(f["shape_ok"] for f in c["files"])
-    assert sorted(f["rank"] for f in c["files"]) == sorted(senders)
+    # a sender opens its log before its first run (mpi_perf.c:479-497)
+    assert sorted(f["rank"] for f in c["files"]) == (sorted(senders) if runs != 0 else [])
 
 
 def test_summary_every_1000_runs():
