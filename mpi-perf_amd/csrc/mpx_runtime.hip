@@ -372,13 +372,25 @@ struct SdmaOps {
     int my_slot, peer_slot;
     u64 tmo;
     int launches = 0;
+    // MPX_SDMA_SIGNAL=kernel|cp: flag store by a one-lane kernel (default) or
+    // by hipStreamWriteValue64.  Waits are always bounded one-lane kernels: a
+    // stream-level wait (hipStreamWaitValue64) cannot time out.
+    bool cp_signal = [] {
+        const char* v = getenv("MPX_SDMA_SIGNAL");
+        return v && !strcmp(v, "cp");
+    }();
 
     int push(long long n, u64 seq) {
         if (n > 0) {
             HIPCK(hipMemcpyAsync(peer.rx, me.tx, (size_t)n, hipMemcpyDeviceToDevice, me.stream));
             ++launches;
         }
-        HIPCK(launch_signal(&peer.mb->flag[my_slot][0], seq, me.stream));
+        if (cp_signal) {
+            // command-processor write, ordered after the copy on this stream
+            HIPCK(hipStreamWriteValue64(me.stream, &peer.mb->flag[my_slot][0], seq, 0));
+        } else {
+            HIPCK(launch_signal(&peer.mb->flag[my_slot][0], seq, me.stream));
+        }
         ++launches;
         return MPX_OK;
     }

@@ -20,7 +20,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "one":
             t = c.copy(0, b, a, n, 10)
             best = max(best, 2 * n * t.launches / t.device_s / 1e9)
         assert c.checksum(a, n) == c.checksum(b, n)
-        print(json.dumps({"variant": os.environ.get("MPX_COPY_VARIANT"), "bytes": n, "hbm_GBps": round(best, 1),
+        print(json.dumps({"variant": os.environ.get("MPX_COPY_VARIANT", "default"), "bytes": n,
+                          "us_per_launch": round(2 * n / best / 1e3, 3), "hbm_GBps": round(best, 1),
                           "grid": t.nwg}), flush=True)
     sys.exit(0)
 
@@ -45,8 +46,16 @@ else:
 sizes = [n]
 if os.environ.get("SWEEP") == "sizes":
     sizes = [1 << k for k in range(12, 31, 2)]
+if os.environ.get("SWEEP") == "cfg2":       # BASELINE config 2: 1 B .. 1 GiB, default variant
+    variants = [None]
+    sizes = [1 << k for k in range(0, 31)]
 for v in variants:
     for size in sizes:
-        p = subprocess.run([sys.executable, __file__, "one", str(size)], env=dict(os.environ, MPX_COPY_VARIANT=v),
-                           capture_output=True, text=True, timeout=120)
+        env = dict(os.environ)
+        if v:
+            env["MPX_COPY_VARIANT"] = v
+        else:
+            env.pop("MPX_COPY_VARIANT", None)
+        p = subprocess.run([sys.executable, __file__, "one", str(size)], env=env, capture_output=True, text=True,
+                           timeout=120)
         print(p.stdout.strip() or json.dumps({"variant": v, "error": p.stderr[-300:]}), flush=True)
