@@ -93,3 +93,34 @@ def test_unidir_without_ppn_raises_sigfpe_like_reference(tmp_path):
     p, recs, side = run(tmp_path, ["-w", "2"] + c["args"])
     assert p.returncode == -8 and c["returncode"] == 8
     assert len(re.findall(r"INFO: ", p.stderr)) == len(c["info"])
+
+
+@pytest.mark.parametrize("name", ["zero_iters", "unidir_wins_over_nonblocking", "zero_runs"])
+def test_degenerate_loops_match_reference(tmp_path, name):
+    c = GOLDEN[name]
+    p, recs, side = run(tmp_path, ["-w", "2"] + c["args"])
+    assert p.returncode == 0, p.stderr[-600:]
+    assert len(recs) == c["n_records"]
+    assert len(list((tmp_path / "logs").glob("tcp-*.log")) if (tmp_path / "logs").exists() else []) == len(c["files"])
+    assert sorted(int(x) for x in re.findall(r"\[Run#: (\d+)\]", p.stderr)) == c["summaries"]
+    if name == "unidir_wins_over_nonblocking":
+        assert {f[4] for f in side} == {"2"}            # unidir mode ran
+
+
+def test_log_rotation_and_ingest_hook(tmp_path):
+    """LOG_REFRESH_TIME_SEC rotation (mpi_perf.c:479-497) with the ingest hook
+    (mpi_perf.c:355-365) called by node-local rank 0 at every open."""
+    hook = tmp_path / "hook.log"
+    env_cmd = f"echo ingest >> {hook}"
+    g1 = tmp_path / "group1"
+    g1.write_text("vm\n")
+    env = dict(os.environ, MPX_PROCESSOR_NAMES="vm,runsc", MPX_LOG_REFRESH_SEC="0.2", MPX_INGEST_CMD=env_cmd)
+    p = subprocess.run([PERF, "-g", "0,0", "-w", "2", "-f", str(g1), "-n", "1", "-p", "1", "-u", "1", "-r", "6",
+                        "-i", "20000", "-b", "8", "-l", str(tmp_path / "logs")], capture_output=True, text=True,
+                       env=env, timeout=120)
+    assert p.returncode == 0, p.stderr[-600:]
+    opened = hook.read_text().count("ingest") if hook.exists() else 0
+    files = list((tmp_path / "logs").glob("tcp-*.log"))
+    assert opened >= 2 and len(files) >= 1          # rotated at least once (names collide within one second)
+    total = sum(len(f.read_text().splitlines()) for f in files)
+    assert 1 <= total <= 5
