@@ -40,7 +40,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 
 HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-XGMI_LINK_PEAK_GBPS = 153.6  # BASELINE.json north_star: ~153 GB/s per xGMI link
+# xGMI: BASELINE.json quotes ~153 GB/s per link.  That is the link's
+# bidirectional figure (MI355X: 7 links x 153.6 GB/s = 1075 GB/s aggregate
+# peer bandwidth, both directions counted), i.e. 76.8 GB/s per direction.  A
+# unidirectional pair uses one direction of its one link, so that is its
+# roofline; the bidirectional figure is reported beside it.
+XGMI_LINK_PEAK_BIDIR_GBPS = 153.6
+XGMI_LINK_PEAK_GBPS = XGMI_LINK_PEAK_BIDIR_GBPS / 2
 
 
 def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:
@@ -180,6 +186,10 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
                 c.close()
             except Exception:  # noqa: BLE001
                 pass
+        # every rank's imports of the others' buffers are closed before any
+        # rank allocates again: a block still imported by a peer cannot be
+        # re-exported (hipIpcGetMemHandle: invalid argument, seen on gfx950)
+        dist.barrier()
         return {"error": err}
     out["validated_rounds"] = len(rounds)
 
@@ -217,6 +227,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / 4000 * 1e6, 3)
     dist.barrier()
     c.close()
+    dist.barrier()   # see above: all imports closed before the next allocation
     return out
 
 
@@ -326,6 +337,8 @@ def main() -> None:
         achieved = res["per_pair_GBps"]
         roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",
                     frac=round(achieved / XGMI_LINK_PEAK_GBPS, 4), traffic=None,
+                    peak_note="one direction of one xGMI link (153.6 GB/s bidirectional per link)",
+                    frac_of_bidirectional_link=round(achieved / XGMI_LINK_PEAK_BIDIR_GBPS, 4),
                     kernel="k_xfer (G1 side)" if engine_used == "kernel" else engine_used,
                     avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
         config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=engine_used,

@@ -489,6 +489,7 @@ __global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
 // launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k_xfer, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
@@ -540,6 +541,7 @@ hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int*
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
     if (grid_out) *grid_out = (int)grid;
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const v4u*>(src),
                        reinterpret_cast<v4u*>(dst), n16, tail);
     return hipGetLastError();
@@ -549,6 +551,7 @@ hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s) {
     size_t grid = (n / 8 + kBlock - 1) / kBlock;
     if (grid > 4096) grid = 4096;
     if (grid < 1) grid = 1;
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k_fill, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<unsigned char*>(p), n,
                        pattern, arg);
     return hipGetLastError();
@@ -558,17 +561,20 @@ hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s)
     size_t grid = (n / 16 + kBlock - 1) / kBlock;
     if (grid > 2048) grid = 2048;
     if (grid < 1) grid = 1;
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k_checksum, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const unsigned char*>(p),
                        n, out_dev);
     return hipGetLastError();
 }
 
 hipError_t launch_signal(u64* flag, u64 value, hipStream_t s) {
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, s, flag, value);
     return hipGetLastError();
 }
 
 hipError_t launch_wait(const u64* flag, u64 value, Status* st, u64 timeout_ticks, hipStream_t s) {
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k_wait, dim3(1), dim3(64), 0, s, flag, value, st, timeout_ticks);
     return hipGetLastError();
 }

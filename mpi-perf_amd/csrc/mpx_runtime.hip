@@ -597,7 +597,11 @@ int mpx_finalize(mpx_ctx* ctx) {
         }
     }
     DBG("finalize: streams drained\n");
-    for (void* p : ctx->ipc_opened) (void)hipIpcCloseMemHandle(p);
+    for (void* p : ctx->ipc_opened) {
+        const hipError_t e = hipIpcCloseMemHandle(p);
+        if (e != hipSuccess) DBG("finalize: hipIpcCloseMemHandle(%p): %s\n", p, hipGetErrorString(e));
+    }
+    (void)hipGetLastError();
     for (int i = 0; i < MPX_MAX_RANKS; ++i) {
         Rank& rk = ctx->r[i];
         if (!rk.local) continue;
@@ -822,6 +826,7 @@ int mpx_rank_export(mpx_ctx* ctx, int rank, void* desc) {
     memcpy(d.bus_id, rk.bus_id, sizeof d.bus_id);
     gethostname(d.host, sizeof d.host - 1);
     DeviceGuard g(rk.dev);
+    DBG("export rank %d: rx %p mb %p (kind %d) dev %d\n", rank, (void*)rk.rx, (void*)rk.mb, rk.mb_kind, rk.dev);
     HIPCK(hipIpcGetMemHandle(&d.rx_handle, rk.rx));
     HIPCK(hipIpcGetMemHandle(&d.mb_handle, rk.mb));
     memset(desc, 0, MPX_RANK_DESC_BYTES);
