@@ -303,7 +303,7 @@ def main() -> None:
         algo = 2 * nbytes   # read B + write B per launch
         achieved = algo / per_launch / 1e9
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None, kernel="k_copy<2,nt,nt,contig>",
+                    frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None, kernel="k_copy<1,nt,nt> (one 16-B unit per lane, n/4 KiB blocks)",
                     avg_launch_us=round(per_launch * 1e6, 2), algorithmic_bytes_per_launch=algo)
         prof = traffic_from_profile(workload)
         if prof and prof.get("bytes") == nbytes:

@@ -1,7 +1,7 @@
 // mpx_kernels.hip — CDNA4 (gfx950) device code of libmpx.
 //
 // Kernels
-//   k_copy      local HBM copy, 16 B per lane, 4 loads in flight   (config 2)
+//   k_copy      local HBM copy, one 16-B unit per lane, one step per block (config 2)
 //   k_xfer      the reference's three transfer loops as ONE persistent launch
 //               per rank: pushes go straight into the peer's HBM over xGMI,
 //               receives are device-side polls of the rank's mailbox
@@ -506,14 +506,18 @@ struct CopyVariant {
     int u, ldnt, stnt, contig;
     copy_fn fn;
 };
-static const CopyVariant kCopyVariants[] = {COPY_VARIANTS(2), COPY_VARIANTS(4), COPY_VARIANTS(8), COPY_VARIANTS(16)};
+static const CopyVariant kCopyVariants[] = {COPY_VARIANTS(1), COPY_VARIANTS(2), COPY_VARIANTS(4), COPY_VARIANTS(8),
+                                            COPY_VARIANTS(16)};
 
-// Default from the tuning sweeps (DESIGN.md "k_copy tuning", profiles/
-// copy_sweep_r01.jsonl): 2 loads in flight per lane, nontemporal loads and
-// stores, one contiguous 8-16 KiB chunk per block, up to 256 blocks per CU.
-// 1 GiB: 6.2-6.4 TB/s of HBM traffic (grid-stride, 16 blocks/CU: 4.5 TB/s).
+// Default from the tuning sweeps (DESIGN.md "k_copy tuning"): ONE 16-B unit
+// per lane and ONE step per block — grid = n/4 KiB workgroups of 256 lanes,
+// no cap (blocks_per_cu = 0), nontemporal loads and stores.  6.51-6.53 TB/s
+// of HBM traffic at 256 MiB, 1 GiB and 4 GiB alike (profiles/
+// r01_copy_lab_onestep.jsonl), against 6.0 / 5.45 TB/s for the earlier
+// contiguous-chunk form (2 loads per lane, 16 KiB per block, 65536 blocks)
+// and 4.76 TB/s for hipMemcpyAsync device-to-device.
 struct CopyConfig {
-    int u = 2, ldnt = 1, stnt = 1, contig = 1, blocks_per_cu = 256;
+    int u = 1, ldnt = 1, stnt = 1, contig = 0, blocks_per_cu = 0;
 };
 
 static CopyConfig copy_config() {
@@ -537,7 +541,9 @@ hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int*
     const size_t n16 = n / 16;
     const unsigned tail = (unsigned)(n & 15);
     size_t grid = (n16 + (size_t)kBlock * cfg.u - 1) / ((size_t)kBlock * cfg.u);
-    const size_t cap = (size_t)256 * (cfg.blocks_per_cu > 0 ? cfg.blocks_per_cu : 16);
+    // blocks_per_cu = 0: one step per block (grid-stride loops then run once);
+    // the cap only bounds gridDim.x, which a 2^31-unit copy stays far below
+    const size_t cap = cfg.blocks_per_cu > 0 ? (size_t)256 * cfg.blocks_per_cu : ((size_t)1 << 30);
     if (grid > cap) grid = cap;
     if (grid < 1) grid = 1;
     if (grid_out) *grid_out = (int)grid;

@@ -1,0 +1,54 @@
+/*
+ * mpx_boot.h — the out-of-band job communicator of mpx_perf's multi-process
+ * mode (one process per rank, started by any launcher: mpiexec, torchrun,
+ * srun).  Pure C over TCP sockets, star topology around rank 0.
+ *
+ * It replaces the MPI collectives the reference calls OUTSIDE its transfer
+ * loops (SURVEY.md §2 call-site table); the loops themselves never touch it:
+ *   mpxb_bcast0         MPI_Bcast of options / group-1 hosts   mpi_perf.c:422-431
+ *   mpxb_allgather      MPI_Allgather of node_info             mpi_perf.c:223-224
+ *   mpxb_barrier        MPI_Barrier                            mpi_perf.c:499,557,579
+ *   mpxb_allreduce_f64  MPI_Allreduce MIN / MAX / SUM          mpi_perf.c:560-562
+ * Every call is collective: all ranks make the same calls in the same order.
+ * Errors return -1 with a message in mpxb_error(); callers abort the job.
+ */
+#ifndef MPX_BOOT_H
+#define MPX_BOOT_H
+
+#include <stddef.h>
+
+typedef struct mpxb mpxb;
+
+/* The launcher's view of this process (first variable set wins):
+ *   rank : MPX_RANK, RANK, PMI_RANK, OMPI_COMM_WORLD_RANK, SLURM_PROCID
+ *   size : MPX_SIZE, WORLD_SIZE, PMI_SIZE, OMPI_COMM_WORLD_SIZE, SLURM_NTASKS
+ *   local: MPX_LOCAL_RANK, LOCAL_RANK, MPI_LOCALRANKID, OMPI_COMM_WORLD_LOCAL_RANK, SLURM_LOCALID
+ * Returns 1 if a launcher was found (rank and size set), else 0 with
+ * *rank = 0, *size = 1, *local = 0. */
+int mpxb_launcher(int *rank, int *size, int *local);
+
+/* Rendezvous address: MPX_BOOTSTRAP="host:port", else MASTER_ADDR and
+ * MASTER_PORT + 1 (torchrun's own store owns MASTER_PORT), else
+ * 127.0.0.1:29571.  Writes host into host[cap]; returns the port. */
+int mpxb_address(char *host, size_t cap);
+
+/* Connect the job: rank 0 listens on host:port, every other rank connects
+ * (retrying until timeout_s).  Returns 0 or -1. */
+int mpxb_init(mpxb **out, int rank, int size, const char *host, int port, double timeout_s);
+void mpxb_finalize(mpxb *b);
+
+int mpxb_rank(const mpxb *b);
+int mpxb_size(const mpxb *b);
+
+/* all[r*bytes .. (r+1)*bytes) = rank r's `mine`, on every rank */
+int mpxb_allgather(mpxb *b, const void *mine, void *all, size_t bytes);
+/* rank 0's buf[0:bytes) to every rank */
+int mpxb_bcast0(mpxb *b, void *buf, size_t bytes);
+int mpxb_barrier(mpxb *b);
+/* min / max / sum of one double per rank (any output may be NULL); every
+ * rank gets bit-identical results (reduced in rank order) */
+int mpxb_allreduce_f64(mpxb *b, double v, double *mn, double *mx, double *sum);
+
+const char *mpxb_error(void);
+
+#endif

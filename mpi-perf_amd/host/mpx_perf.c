@@ -1,18 +1,28 @@
 /*
- * mpx_perf.c — mpi_perf for the GPUs of one MI355X node.
+ * mpx_perf.c — mpi_perf for MI355X GPUs.
  *
  * Same command line, group/peer rule, run loop, timing, CSV records and log
- * rotation as /root/reference/mpi_perf.c:367-582, but the ranks are host
- * threads of one process, one per GPU, and the transfer loop is libmpx's
- * mpx_xfer_ex (kernel / SDMA / RCCL engines over xGMI) instead of MPI p2p.
+ * rotation as /root/reference/mpi_perf.c:367-582; the transfer loop is
+ * libmpx's mpx_xfer_ex (kernel / SDMA / RCCL engines over xGMI) instead of
+ * MPI point-to-point.  Two ways to start the ranks, same flags:
  *
- *   mpirun -np N --map-by ppr:P:node mpi_perf -f g1 -n 1 -p P ...   (reference)
- *   mpx_perf -w N -f g1 -n 1 -p P ...                                 (here)
+ *   threads   mpx_perf -w N -f g1 -n 1 -p P ...
+ *             one process, one host thread per rank (and GPU).
+ *   processes mpiexec -n N mpx_perf -f g1 -n 1 -p P ...      (or torchrun, srun)
+ *             one process per rank, exactly the reference's process model
+ *             (mpirun -np N --map-by ppr:P:node mpi_perf ...).  The launcher's
+ *             rank variables are read by mpx_boot_launcher(); the collectives
+ *             the reference makes outside its loops (Bcast, Allgather,
+ *             Barrier, Allreduce) run over mpx_boot's TCP star.  Ranks of one
+ *             node map each other's rx and mailbox through IPC (kernel and
+ *             SDMA engines); the RCCL engine also spans nodes.
+ *             MPX_LAUNCH=threads forces the threads mode under a launcher.
  *
- * Ranks [k*P, (k+1)*P) form virtual host k, named "<node>-<k>" (the
- * processor name each rank matches against the -f file, mpi_perf.c:433-444;
- * MPX_PROCESSOR_NAMES="a,a,b,b" overrides).  With -a 1 every run is one round
- * of the circle-method all-pairs schedule instead of the fixed pairing.
+ * Processor names (the string matched against the -f file, mpi_perf.c:433-444):
+ * MPX_PROCESSOR_NAMES="a,a,b,b" (indexed by world rank) if set; else, when the
+ * ranks span several hosts, the host name, like MPI_Get_processor_name; else
+ * (one host) virtual host k = "<host>-<k>" for ranks [k*P, (k+1)*P).  With
+ * -a 1 every run is one round of the circle-method all-pairs schedule.
  */
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
@@ -29,6 +39,7 @@
 #include <unistd.h>
 
 #include "../../include/mpx.h"
+#include "mpx_boot.h"
 #include "mpx_host.h"
 
 /* MPI_CHECK analogue, mpi_perf.c:55-64: print and exit(EXIT_FAILURE) */
@@ -55,6 +66,7 @@ static int world;
 static mpx_ctx *ctx;
 static int dev_of[MPXH_MAX_RANKS];
 static char name_of[MPXH_MAX_RANKS][MPXH_MAX_HOST];
+static char host_of[MPXH_MAX_RANKS][MPXH_MAX_HOST]; /* real host names */
 static char ip_of[MPXH_MAX_RANKS][MPXH_MAX_HOST];
 static int group_of[MPXH_MAX_RANKS], grank_of[MPXH_MAX_RANKS], gsize_of[MPXH_MAX_RANKS], peer_of[MPXH_MAX_RANKS];
 static void *tx_of[MPXH_MAX_RANKS], *rx_of[MPXH_MAX_RANKS];
@@ -66,6 +78,13 @@ static int sizes[40], nsizes;
 /* LOG_REFRESH_TIME_SEC (mpi_perf.c:16); MPX_LOG_REFRESH_SEC overrides it for tests */
 static double log_refresh_sec = MPXH_LOG_REFRESH_SEC;
 
+/* processes mode */
+static int procs;            /* 1: one process per rank under a launcher */
+static int me;               /* this process's world rank (processes mode) */
+static int local_rank;       /* its node-local rank */
+static int multi_host;       /* the ranks span more than one host */
+static mpxb *boot;
+
 static double wtime(void) /* MPI_Wtime */
 {
     struct timespec ts;
@@ -73,14 +92,56 @@ static double wtime(void) /* MPI_Wtime */
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-static void barrier(void) { pthread_barrier_wait(&bar); }
+static int is_root(void) { return !procs || me == 0; }
 
-/* kusto_injest, mpi_perf.c:355-365: only node-local rank 0; the command is
-   site configuration here (MPX_INGEST_CMD) instead of a hard-coded path */
+static void boot_failed(void)
+{
+    fprintf(stderr, "mpx_perf: job communicator failed: %s\n", mpxb_error());
+    mpx_abort();
+}
+
+/* MPI_Barrier, mpi_perf.c:499,557,579 */
+static void barrier(void)
+{
+    if (procs) {
+        if (mpxb_barrier(boot) != 0) boot_failed();
+    } else {
+        pthread_barrier_wait(&bar);
+    }
+}
+
+/* every rank learns every rank's tx checksums (check mode's expected values) */
+static void share_tx_checksums(int r, uint64_t s, uint64_t s1)
+{
+    if (procs) {
+        uint64_t mine[2] = {s, s1}, all[MPXH_MAX_RANKS][2];
+        if (mpxb_allgather(boot, mine, all, sizeof mine) != 0) boot_failed();
+        for (int q = 0; q < world; ++q) {
+            txsum_of[q] = all[q][0];
+            txsum1_of[q] = all[q][1];
+        }
+        return;
+    }
+    barrier(); /* nobody still reads last run's values */
+    txsum_of[r] = s;
+    txsum1_of[r] = s1;
+    barrier();
+}
+
+/* node-local rank of rank r: the ingest hook runs on node-local rank 0 only
+   (OMPI_COMM_WORLD_LOCAL_RANK, mpi_perf.c:355-365, :378-384) */
+static int node_local(int r)
+{
+    if (procs && multi_host) return local_rank;
+    return r % (opt.ppn > 0 ? opt.ppn : 1);
+}
+
+/* kusto_injest, mpi_perf.c:355-365: the command is site configuration here
+   (MPX_INGEST_CMD) instead of a hard-coded path */
 static void ingest_hook(int rank)
 {
     const char *cmd = getenv("MPX_INGEST_CMD");
-    if (rank % (opt.ppn > 0 ? opt.ppn : 1) != 0 || !cmd || !*cmd) return;
+    if (node_local(rank) != 0 || !cmd || !*cmd) return;
     if (system(cmd) == -1) fprintf(stderr, "ingest hook failed: %s\n", strerror(errno));
 }
 
@@ -152,10 +213,10 @@ static void *rank_main(void *arg)
             xo.timeout_ms = (uint32_t)opt.timeout_ms;
             if (opt.check && !opt.use_dotnet) {
                 /* expected payloads: the peer's tx, read after every fill */
-                barrier();
-                MPX_CHECK(mpx_checksum(ctx, dev_of[r], tx_of[r], (size_t)B, &txsum_of[r]));
-                MPX_CHECK(mpx_checksum(ctx, dev_of[r], tx_of[r], 1, &txsum1_of[r]));
-                barrier();
+                uint64_t s, s1;
+                MPX_CHECK(mpx_checksum(ctx, dev_of[r], tx_of[r], (size_t)B, &s));
+                MPX_CHECK(mpx_checksum(ctx, dev_of[r], tx_of[r], 1, &s1));
+                share_tx_checksums(r, s, s1);
                 xo.check = 1;
                 xo.expect_checksum = txsum_of[peer];
                 xo.expect_ack = txsum1_of[peer];
@@ -200,13 +261,21 @@ static void *rank_main(void *arg)
             time_of[r] = my_time;
             barrier(); /* MPI_Barrier, mpi_perf.c:557 */
             const double t_end = wtime();
-            if (r == 0 && (run_idx % 1000 == 0)) { /* Allreduce MIN/MAX/SUM + print, :560-568 */
-                double mn = time_of[0], mx = time_of[0], sum = 0;
+            /* Allreduce MIN/MAX/SUM, mpi_perf.c:560-562 (every run, every rank) */
+            double mn = my_time, mx = my_time, sum = my_time;
+            if (procs) {
+                if (mpxb_allreduce_f64(boot, my_time, &mn, &mx, &sum) != 0) boot_failed();
+            } else if (r == 0) {
+                /* the other threads cannot overwrite time_of before rank 0
+                   reaches the next run's barrier */
+                sum = 0;
                 for (int q = 0; q < world; ++q) {
                     if (time_of[q] < mn) mn = time_of[q];
                     if (time_of[q] > mx) mx = time_of[q];
                     sum += time_of[q];
                 }
+            }
+            if (r == 0 && (run_idx % 1000 == 0)) { /* mpi_perf.c:564-568 */
                 char line[256];
                 mpxh_format_summary(line, sizeof line, run_idx, t_end - t_start, mn, mx, sum, world);
                 fputs(line, stderr);
@@ -218,53 +287,185 @@ static void *rank_main(void *arg)
     return NULL;
 }
 
+/* ---- processes mode: the reference's once-per-job collectives ------------ */
+
+/* MPI_Bcast of the options (with rank 0's UUID) and of the group-1 host
+   lines, mpi_perf.c:422-431.  Rank 0 has read the -f file. */
+static char *share_options_and_group1(char *group1)
+{
+    if (mpxb_bcast0(boot, &opt, sizeof opt) != 0) boot_failed();
+    int ok = group1 != NULL;
+    if (mpxb_bcast0(boot, &ok, sizeof ok) != 0) boot_failed();
+    if (!ok) mpx_abort(); /* rank 0 printed "cannot open group1 file" */
+    if (me != 0) group1 = (char *)calloc((size_t)(opt.group_size > 0 ? opt.group_size : 1), MPXH_MAX_HOST);
+    if (mpxb_bcast0(boot, group1, (size_t)opt.group_size * MPXH_MAX_HOST) != 0) boot_failed();
+    return group1;
+}
+
+/* node_info Allgather (mpi_perf.c:215-224): host name, GPU, IP of every rank */
+typedef struct {
+    char host[MPXH_MAX_HOST];
+    char ip[MPXH_MAX_HOST];
+    int32_t dev;
+} node_info;
+
+static void share_node_info(const char *node, const char *ip, int dev)
+{
+    node_info mine, all[MPXH_MAX_RANKS];
+    memset(&mine, 0, sizeof mine);
+    snprintf(mine.host, sizeof mine.host, "%s", node);
+    snprintf(mine.ip, sizeof mine.ip, "%s", ip);
+    mine.dev = dev;
+    if (mpxb_allgather(boot, &mine, all, sizeof mine) != 0) boot_failed();
+    for (int q = 0; q < world; ++q) {
+        memcpy(host_of[q], all[q].host, MPXH_MAX_HOST);
+        memcpy(ip_of[q], all[q].ip, MPXH_MAX_HOST);
+        dev_of[q] = all[q].dev;
+        if (strcmp(host_of[q], host_of[0]) != 0) multi_host = 1;
+    }
+}
+
+/* Peers this rank transfers with: its fixed peer, or everyone (-a 1). */
+static int needs_peer(int q)
+{
+    if (q == me) return 0;
+    return opt.all_pairs || peer_of[me] == q;
+}
+
+/* Map the peers' buffers (kernel / SDMA engines: IPC within one node) or
+   join the RCCL communicator (rank 0's unique id, any number of nodes). */
+static void connect_ranks(void)
+{
+    if (opt.engine == MPX_ENGINE_RCCL) {
+        unsigned char id[MPX_RCCL_ID_BYTES] = {0};
+        if (me == 0) MPX_CHECK(mpx_rccl_get_unique_id(id));
+        if (mpxb_bcast0(boot, id, sizeof id) != 0) boot_failed();
+        MPX_CHECK(mpx_rccl_init_rank(ctx, me, world, id));
+        return;
+    }
+    for (int q = 0; q < world; ++q) {
+        if (needs_peer(q) && strcmp(host_of[q], host_of[me]) != 0) {
+            fprintf(stderr,
+                    "rank %d (%s) and rank %d (%s) are on different hosts: the %s engine needs both on one node "
+                    "(use -e rccl)\n",
+                    me, host_of[me], q, host_of[q], mpxh_engine_name(opt.engine));
+            mpx_abort();
+        }
+    }
+    static unsigned char all[MPXH_MAX_RANKS][MPX_RANK_DESC_BYTES];
+    unsigned char mine[MPX_RANK_DESC_BYTES];
+    MPX_CHECK(mpx_rank_export(ctx, me, mine));
+    if (mpxb_allgather(boot, mine, all, sizeof mine) != 0) boot_failed();
+    for (int q = 0; q < world; ++q)
+        if (q != me && strcmp(host_of[q], host_of[me]) == 0) MPX_CHECK(mpx_rank_import(ctx, q, all[q]));
+}
+
 int main(int argc, char **argv)
 {
+    int lrank = 0, lsize = 1;
+    const char *launch = getenv("MPX_LAUNCH");
+    const int found = mpxb_launcher(&lrank, &lsize, &local_rank);
+    procs = found && lsize > 1 && !(launch && !strcmp(launch, "threads"));
+    me = procs ? lrank : 0;
+
     mpxh_defaults(&opt);
     const int pst = mpxh_parse_args(&opt, argc, argv);
     if (pst == MPXH_PARSE_USAGE) {
-        mpxh_print_usage(stderr);
+        if (is_root()) mpxh_print_usage(stderr);
         mpx_abort();
     }
     if (pst == MPXH_PARSE_BAD_VALUE) {
-        fprintf(stderr, "bad value for -e / -S\n");
-        mpxh_print_usage(stderr);
+        if (is_root()) {
+            fprintf(stderr, "bad value for -e / -S\n");
+            mpxh_print_usage(stderr);
+        }
         mpx_abort();
     }
-    fprintf(stderr, "UUID: %s\n", opt.uuid); /* mpi_perf.c:338 */
+    if (is_root()) fprintf(stderr, "UUID: %s\n", opt.uuid); /* mpi_perf.c:338 */
 #ifdef REPORT_BANDWIDTH
     report_bandwidth = 1;
 #else
     report_bandwidth = getenv("MPX_REPORT_BANDWIDTH") != NULL;
 #endif
-
     if (getenv("MPX_LOG_REFRESH_SEC")) log_refresh_sec = atof(getenv("MPX_LOG_REFRESH_SEC"));
-    world = opt.world > 0 ? opt.world : (opt.ppn > 0 ? 2 * opt.ppn : 2);
-    if (world > MPXH_MAX_RANKS || world > MPX_MAX_RANKS) {
-        fprintf(stderr, "at most %d ranks\n", MPXH_MAX_RANKS);
-        mpx_abort();
+
+    if (procs) {
+        world = lsize;
+        if (world > MPXH_MAX_RANKS || world > MPX_MAX_RANKS || lrank < 0 || lrank >= world) {
+            if (is_root()) fprintf(stderr, "at most %d ranks\n", MPXH_MAX_RANKS);
+            mpx_abort();
+        }
+        if (opt.world > 0 && opt.world != world) {
+            if (is_root()) fprintf(stderr, "-w %d but the launcher started %d ranks\n", opt.world, world);
+            mpx_abort();
+        }
+    } else {
+        world = opt.world > 0 ? opt.world : (opt.ppn > 0 ? 2 * opt.ppn : 2);
+        if (world > MPXH_MAX_RANKS || world > MPX_MAX_RANKS) {
+            fprintf(stderr, "at most %d ranks\n", MPXH_MAX_RANKS);
+            mpx_abort();
+        }
     }
-    const int v = mpxh_validate(&opt, world, stderr); /* mpi_perf.c:399-403 */
+    /* rank 0 validates (mpi_perf.c:399-403); the others see the same values */
+    FILE *quiet = is_root() ? stderr : fopen("/dev/null", "w");
+    const int v = mpxh_validate(&opt, world, quiet ? quiet : stderr);
     if (v == 2) raise(SIGFPE);
     if (v) mpx_abort();
-    char *group1 = mpxh_read_group1(opt.group1_hostfile, opt.group_size);
-    if (!group1) {
-        fprintf(stderr, "cannot open group1 file: %s\n", opt.group1_hostfile);
-        mpx_abort();
+    char *group1 = NULL;
+    if (is_root()) {
+        group1 = mpxh_read_group1(opt.group1_hostfile, opt.group_size);
+        if (!group1) {
+            fprintf(stderr, "cannot open group1 file: %s\n", opt.group1_hostfile);
+            if (!procs) mpx_abort();
+        }
     }
     if (opt.all_pairs && (world < 2 || (world & 1))) {
-        fprintf(stderr, "-a 1 needs an even number of ranks (-w)\n");
+        if (is_root()) fprintf(stderr, "-a 1 needs an even number of ranks\n");
         mpx_abort();
     }
 
-    /* processor names and the group/peer rule, mpi_perf.c:433-458 */
+    /* this process's host, IP and (processes mode) GPU */
     char node[MPXH_MAX_HOST] = {0};
     gethostname(node, sizeof node - 1);
     char node_ip[MPXH_MAX_HOST] = "127.0.0.1";
     if (mpxh_ipv4(node, node_ip, sizeof node_ip) != 0) snprintf(node_ip, sizeof node_ip, "127.0.0.1");
+    int ndev = world;
+    int gl[MPXH_MAX_RANKS];
+    const int ngl = opt.gpus[0] ? mpxh_parse_gpu_list(opt.gpus, gl, MPXH_MAX_RANKS) : 0;
+
+    if (procs) {
+        char bhost[MPXH_MAX_HOST];
+        const int port = mpxb_address(bhost, sizeof bhost);
+        const char *tmo = getenv("MPX_BOOTSTRAP_TIMEOUT");
+        if (mpxb_init(&boot, me, world, bhost, port, tmo ? atof(tmo) : 120.0) != 0) boot_failed();
+        group1 = share_options_and_group1(group1);
+        /* GPU of this rank: -g indexed by node-local rank, else the node-local
+           rank itself (checked against the visible GPUs after the pairing, so
+           the configuration errors come first, as in the reference) */
+        int dev = local_rank;
+        if (opt.gpus[0]) {
+            if (ngl <= local_rank) {
+                fprintf(stderr, "-g lists no GPU for node-local rank %d\n", local_rank);
+                mpx_abort();
+            }
+            dev = gl[local_rank];
+        }
+        char ip[MPXH_MAX_HOST];
+        snprintf(ip, sizeof ip, "%s:gpu%d", node_ip, dev);
+        share_node_info(node, ip, dev);
+    } else {
+        for (int r = 0; r < world; ++r) snprintf(host_of[r], MPXH_MAX_HOST, "%s", node);
+    }
+
+    /* processor names and the group/peer rule, mpi_perf.c:433-458 */
     const char *names_env = getenv("MPX_PROCESSOR_NAMES");
     for (int r = 0; r < world; ++r) {
-        mpxh_processor_name(name_of[r], node, r, opt.ppn, names_env);
+        if (names_env && *names_env)
+            mpxh_processor_name(name_of[r], host_of[r], r, opt.ppn, names_env);
+        else if (multi_host)
+            snprintf(name_of[r], MPXH_MAX_HOST, "%s", host_of[r]); /* MPI_Get_processor_name */
+        else
+            mpxh_processor_name(name_of[r], host_of[r], r, opt.ppn, NULL);
         group_of[r] = mpxh_in_group1(name_of[r], group1, opt.group_size);
     }
     mpxh_pairing(world, group_of, grank_of, gsize_of, peer_of);
@@ -272,41 +473,44 @@ int main(int argc, char **argv)
 
     if (!opt.all_pairs) {
         for (int r = 0; r < world; ++r) {
-            if (peer_of[r] < 0) { /* get_ipaddress(NULL peer host) aborts, mpi_perf.c:180-184 */
+            if (peer_of[r] < 0 && (!procs || r == me)) { /* get_ipaddress(NULL peer), mpi_perf.c:180-184 */
                 fprintf(stderr, "getaddrinfo error: rank %d (%s) has no peer in the other group\n", r, name_of[r]);
                 mpx_abort();
             }
         }
+        /* a rank whose peer is missing aborts the whole job (MPI_Abort) */
+        for (int r = 0; r < world; ++r)
+            if (peer_of[r] < 0) mpx_abort();
     }
-
-    /* the .NET mode only prints launcher lines (mpi_perf.c:147-168) and, like
-       the reference, allocates nothing: it needs no GPU */
-    int ndev = world;
-    if (!opt.use_dotnet) MPX_CHECK(mpx_device_count(&ndev));
-    if (opt.gpus[0]) {
-        if (mpxh_parse_gpu_list(opt.gpus, dev_of, MPXH_MAX_RANKS) < world) {
-            fprintf(stderr, "-g lists fewer GPUs than ranks (%d)\n", world);
-            mpx_abort();
+    if (!procs) { /* threads mode: rank r on GPU -g[r], else r mod #GPUs */
+        if (!opt.use_dotnet) MPX_CHECK(mpx_device_count(&ndev));
+        if (opt.gpus[0]) {
+            if (ngl < world) {
+                fprintf(stderr, "-g lists fewer GPUs than ranks (%d)\n", world);
+                mpx_abort();
+            }
+            for (int r = 0; r < world; ++r) dev_of[r] = gl[r];
+        } else {
+            for (int r = 0; r < world; ++r) dev_of[r] = r % ndev;
         }
-    } else {
-        for (int r = 0; r < world; ++r) dev_of[r] = r % ndev;
-    }
-    for (int r = 0; r < world; ++r) {
-        if (dev_of[r] >= ndev) {
-            fprintf(stderr, "rank %d: GPU %d not visible (%d GPUs)\n", r, dev_of[r], ndev);
-            mpx_abort();
+        for (int r = 0; r < world; ++r) {
+            if (dev_of[r] >= ndev) {
+                fprintf(stderr, "rank %d: GPU %d not visible (%d GPUs)\n", r, dev_of[r], ndev);
+                mpx_abort();
+            }
+            snprintf(ip_of[r], sizeof ip_of[r], "%s:gpu%d", node_ip, dev_of[r]);
         }
-        snprintf(ip_of[r], sizeof ip_of[r], "%s:gpu%d", node_ip, dev_of[r]);
     }
     if (!opt.all_pairs) {
         for (int r = 0; r < world; ++r) {
+            if (procs && r != me) continue; /* every rank prints its own line, mpi_perf.c:460-461 */
             char line[1024];
             const int p = peer_of[r];
             mpxh_format_info(line, sizeof line, name_of[r], r, world, group_of[r], gsize_of[r], grank_of[r], p,
                              ip_of[r], name_of[p], ip_of[p]);
             fputs(line, stderr);
         }
-    } else {
+    } else if (is_root()) {
         for (int rd = 0; rd < world - 1; ++rd) {
             int pairs[MPXH_MAX_RANKS / 2][2];
             const int np = mpxh_round_pairs(world, rd, pairs);
@@ -326,16 +530,38 @@ int main(int argc, char **argv)
     for (int i = 0; i < nsizes; ++i)
         if (sizes[i] > maxb) maxb = sizes[i];
 
+    if (procs && !opt.use_dotnet) {
+        MPX_CHECK(mpx_device_count(&ndev));
+        if (dev_of[me] >= ndev) {
+            fprintf(stderr, "rank %d: GPU %d not visible (%d GPUs; -g maps node-local ranks to GPUs)\n", me,
+                    dev_of[me], ndev);
+            mpx_abort();
+        }
+    }
     if (opt.logfolder[0]) mkdir(opt.logfolder, 0755);
-    if (!opt.use_dotnet) MPX_CHECK(mpx_init(world, opt.engine, &ctx));
     if (!opt.use_dotnet) { /* allocate_tx_rx_buffers, mpi_perf.c:463-468 */
+        MPX_CHECK(mpx_init(world, opt.engine, &ctx));
         for (int r = 0; r < world; ++r) {
+            if (procs && r != me) continue;
             MPX_CHECK(mpx_alloc(ctx, dev_of[r], (size_t)maxb, &tx_of[r]));
             MPX_CHECK(mpx_alloc(ctx, dev_of[r], (size_t)maxb, &rx_of[r]));
             MPX_CHECK(mpx_fill(ctx, dev_of[r], rx_of[r], (size_t)maxb, MPX_FILL_BYTE, 0));
             MPX_CHECK(mpx_rank_attach(ctx, r, dev_of[r], tx_of[r], rx_of[r], (size_t)maxb));
         }
-        if (opt.engine == MPX_ENGINE_RCCL) MPX_CHECK(mpx_rccl_init_all(ctx));
+        if (procs)
+            connect_ranks();
+        else if (opt.engine == MPX_ENGINE_RCCL)
+            MPX_CHECK(mpx_rccl_init_all(ctx));
+    }
+
+    if (procs) {
+        barrier();
+        rank_main((void *)(intptr_t)me);
+        barrier(); /* MPI_Barrier, mpi_perf.c:579: no peer still maps our buffers */
+        if (ctx) MPX_CHECK(mpx_finalize(ctx)); /* frees tx/rx too */
+        barrier();
+        mpxb_finalize(boot);
+        return 0;
     }
 
     pthread_barrier_init(&bar, NULL, (unsigned)world);

@@ -124,3 +124,66 @@ def test_log_rotation_and_ingest_hook(tmp_path):
     assert opened >= 2 and len(files) >= 1          # rotated at least once (names collide within one second)
     total = sum(len(f.read_text().splitlines()) for f in files)
     assert 1 <= total <= 5
+
+
+# ---- processes mode: one mpx_perf process per rank (the reference's model) --
+def run_procs(tmp_path, args, n, names, lines=("vm",)):
+    """n mpx_perf processes on GPU 0 (launcher variables MPX_RANK/MPX_SIZE,
+    -g maps every node-local rank to GPU 0); IPC-mapped peers."""
+    import socket
+    g1 = tmp_path / "group1"
+    g1.write_text("".join(x + "\n" for x in lines))
+    logs = tmp_path / "logs"
+    argv = [a.replace("@G1", str(g1)).replace("@LOGS", str(logs)) for a in args]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ps = []
+    for r in range(n):
+        env = dict(os.environ, MPX_RANK=str(r), MPX_SIZE=str(n), MPX_LOCAL_RANK=str(r), MPX_PROCESSOR_NAMES=names,
+                   MPX_BOOTSTRAP=f"127.0.0.1:{port}", MPX_BOOTSTRAP_TIMEOUT="60")
+        ps.append(subprocess.Popen([PERF, "-g", ",".join(["0"] * n), "-t", "5000"] + argv, stdout=subprocess.PIPE,
+                                   stderr=subprocess.PIPE, text=True, env=env))
+    errs = [p.communicate(timeout=120)[1] for p in ps]
+    recs, side = [], []
+    for f in sorted(glob.glob(str(logs / "tcp-*.log"))):
+        recs += [line.rstrip("\n").split(",") for line in open(f)]
+    for f in sorted(glob.glob(str(logs / "gpu-*.csv"))):
+        side += [line.rstrip("\n").split(",") for line in open(f)][1:]
+    return [p.returncode for p in ps], "".join(errs), recs, side
+
+
+@pytest.mark.parametrize("engine,name", [("kernel", "pingpong_p1_b456131_i3"), ("kernel", "unidir_p2_b4096_i7"),
+                                         ("kernel", "nonblocking_p2_b8_i10"), ("sdma", "pingpong_p1_b456131_i3")])
+def test_processes_mode_records_match_reference_run(tmp_path, engine, name):
+    c = GOLDEN[name]
+    names = ",".join(["vm"] * c["ppn"] + ["runsc"] * c["ppn"])
+    rcs, err, recs, side = run_procs(tmp_path, c["args"] + ["-e", engine, "-c", "1"], c["np"], names)
+    assert rcs == [0] * c["np"], err[-800:]
+    assert len(recs) == c["n_records"]
+    ref = sorted((r["rank"], r["vmcount"], r["flows"], r["buffer_size"], r["num_buffers"], r["run_id"])
+                 for r in c["records"])
+    mine = sorted((int(f[2]), int(f[3]), int(f[6]), int(f[7]), int(f[8]), int(f[10])) for f in recs)
+    assert mine == ref
+    assert len({f[1] for f in recs}) == 1             # one JobId: rank 0's UUID, broadcast
+    info = re.findall(r"INFO: (\S+), rank (\d+) out of (\d+) ranks, my_group: (\d), group_size: (\d+), "
+                      r"group_rank: (\d+), my_peer: (-?\d+)", err)
+    assert sorted((int(x[1]), int(x[3]), int(x[4]), int(x[5]), int(x[6])) for x in info) == \
+        sorted((d["rank"], d["group"], d["group_size"], d["group_rank"], d["peer"]) for d in c["info"])
+    for f in side:
+        assert f[3] == engine
+        if f[4] != "1":
+            assert int(f[16]) == 0 and int(f[15]) == int(f[9])
+
+
+def test_processes_mode_all_pairs_seeded_payloads(tmp_path):
+    rcs, err, recs, side = run_procs(tmp_path, ["-a", "1", "-f", "@G1", "-n", "1", "-p", "2", "-u", "1", "-r", "7",
+                                                "-i", "5", "-b", "300001", "-c", "2", "-l", "@LOGS"], 4,
+                                     "vm,vm,runsc,runsc")
+    assert rcs == [0, 0, 0, 0], err[-800:]
+    assert len(re.findall(r"ROUND (\d+): ", err)) == 3
+    assert len(recs) == 6 * 2
+    from mpx.schedule import all_pairs_rounds
+    assert {(int(f[2]), int(f[6])) for f in side} == {p for rnd in all_pairs_rounds(4) for p in rnd}
+    assert all(int(f[16]) == 0 and int(f[15]) == 5 for f in side)
