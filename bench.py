@@ -231,6 +231,22 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     return out
 
 
+def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
+                        extras: dict) -> tuple[dict, str]:
+    """pairs_bench on `engine`; if the kernel engine fails (payload
+    validation or a device timeout on any rank), measure the SDMA engine
+    instead and say so: an explicit, labelled fallback, never a silent one."""
+    res = pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync)
+    engine_used = engine
+    if res.get("error") and engine == "kernel":
+        fb = pairs_bench(mpx, torch, dist, "sdma", rank, world, dev, nbytes, iters, steps, warmup, barrier_sync)
+        extras["kernel_engine_error"] = res["error"]
+        res, engine_used = fb, "sdma (fallback: kernel engine failed validation)"
+    if res.get("error"):
+        raise SystemExit(f"pairs bench failed: {res['error']}")
+    return res, engine_used
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -238,7 +254,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--engine", default="kernel", choices=["kernel", "sdma", "rccl"])
     ap.add_argument("--bytes", type=int, default=0, help="message bytes (default: 1 GiB at N=1, 4 MiB at N>1)")
-    ap.add_argument("--iters", type=int, default=0, help="transfers per step (default 10 at N=1, 100 at N>1)")
+    ap.add_argument("--iters", type=int, default=0, help="transfers per step (default 10 at N=1, 500 at N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
@@ -251,7 +267,7 @@ def main() -> None:
 
     one = world == 1
     nbytes = args.bytes or ((1 << 30) if one else (4 << 20))
-    iters = args.iters or (10 if one else 100)
+    iters = args.iters or (10 if one else 500)
 
     # CPU baseline first, before this process touches the GPU
     cpu = None
@@ -321,18 +337,8 @@ def main() -> None:
     else:
         workload = "all_pairs_rounds_unidir"
         metric_unit = "GB/s"
-        res = pairs_bench(mpx, torch, dist, args.engine, rank, world, dev, nbytes, iters, args.steps, args.warmup,
-                          barrier_sync)
-        engine_used = args.engine
-        if res.get("error") and args.engine == "kernel":
-            # explicit, labelled fallback: the kernel engine failed payload
-            # validation or timed out on this node; measure the SDMA engine
-            fb = pairs_bench(mpx, torch, dist, "sdma", rank, world, dev, nbytes, iters, args.steps, args.warmup,
-                             barrier_sync)
-            extras["kernel_engine_error"] = res["error"]
-            res, engine_used = fb, "sdma (fallback: kernel engine failed validation)"
-        if res.get("error"):
-            raise SystemExit(f"pairs bench failed: {res['error']}")
+        res, engine_used = pairs_with_fallback(mpx, torch, dist, args.engine, rank, world, dev, nbytes, iters,
+                                               args.steps, args.warmup, barrier_sync, extras)
         elapsed, total = res["elapsed"], res["total"]
         achieved = res["per_pair_GBps"]
         roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",

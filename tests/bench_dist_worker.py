@@ -1,0 +1,110 @@
+"""One rank of tests/test_bench_dist.py: runs bench.py's N>1 orchestration
+(pairs_with_fallback -> pairs_bench) over a gloo process group on CPU, with
+a TEST-ONLY stand-in for the mpx binding that records every call.  The stand-in
+never replaces libmpx in bench.py or anywhere else: it exists only here, to
+check the multi-rank logic (round schedule, peer descriptors, expected
+checksums, error agreement, fallback, max-over-ranks timing) without a GPU.
+
+    python bench_dist_worker.py <rank> <world> <port> <scenario> <outdir>
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import bench  # noqa: E402
+
+rank, world, port, scenario, outdir = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4],
+                                       sys.argv[5])
+
+
+class Timing:
+    def __init__(self, wall_s, device_s):
+        self.wall_s, self.device_s = wall_s, device_s
+
+
+class FakeError(RuntimeError):
+    pass
+
+
+class FakeMpx:
+    """Mirror of the mpx binding's surface that bench.pairs_bench uses."""
+    MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
+    FILL_SPLITMIX = 1
+    PATTERN_SEED = 0x6D70695F70657266
+    log = []
+
+    @staticmethod
+    def pattern_key(seed, src, dst, it):
+        return (seed ^ (src << 56) ^ (dst << 48) ^ (it << 24)) & 0xFFFFFFFFFFFFFFFF
+
+    @staticmethod
+    def rccl_unique_id():
+        return b"uid-from-rank-0"
+
+    class Context:
+        def __init__(self, nranks, engine):
+            self.engine = engine
+            self.nranks = nranks
+            self.filled = None
+            FakeMpx.log.append(["init", engine, nranks])
+
+        def alloc(self, dev, n):
+            return ("buf", dev, n)
+
+        def fill(self, b, n, pattern, key):
+            self.filled = key
+
+        def attach(self, r, dev, tx, rx, n):
+            FakeMpx.log.append(["attach", r, dev, n])
+
+        def export(self, r):
+            return f"desc-of-{r}".encode()
+
+        def checksum(self, b, n):
+            return (self.filled * 31 + n) & 0xFFFFFFFFFFFFFFFF     # a function of this rank's tx
+
+        def import_rank(self, r, desc):
+            if scenario == "import_fails" and rank == 1:
+                raise FakeError(f"cannot map rank {r}")
+            assert desc == f"desc-of-{r}".encode(), (r, desc)
+            FakeMpx.log.append(["import", r])
+
+        def rccl_init_rank(self, r, n, uid):
+            assert uid == b"uid-from-rank-0"
+            FakeMpx.log.append(["rccl_init", r, n])
+
+        def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,
+                 timeout_ms=0):
+            if check_payload and self.engine == "kernel" and scenario == "kernel_fails_validation" and rank == 0:
+                raise FakeError("payload checksum mismatch")
+            FakeMpx.log.append(["xfer", self.engine, mode, group, me, peer, iters, n, bool(check_payload), expect,
+                                expect_ack])
+            time.sleep(0.002)
+            return Timing(0.002, 0.001 * (1 + me))
+
+        def close(self):
+            FakeMpx.log.append(["close", self.engine])
+
+
+dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+extras = {}
+out = {"rank": rank}
+try:
+    res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, 4096, 7, 5, 2,
+                                          dist.barrier, extras)
+    out.update(res=res, engine_used=used, extras=extras)
+except SystemExit as e:
+    out.update(exit=str(e))
+out["log"] = FakeMpx.log
+with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+    json.dump(out, f)
+dist.barrier()
+dist.destroy_process_group()

@@ -1,0 +1,99 @@
+"""bench.py's N > 1 path (one process per GPU) rehearsed on CPU: world size 2
+and 4 over gloo, with a test-only stand-in for the libmpx binding
+(tests/bench_dist_worker.py).  Checks what the GPU run relies on but cannot
+show on a one-GPU box: every rank follows the same circle-method round each
+step and its peer follows the mirror role; each rank maps every other rank's
+descriptor; the expected checksums handed to each validation transfer are the
+PEER's tx checksums; an error on one rank reaches every rank (no hang); the
+kernel engine's failure falls back to SDMA with a label; timing is the max
+over ranks."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "mpi-perf_amd"))
+from mpx.schedule import all_pairs_rounds, round_role  # noqa: E402
+
+SEED = 0x6D70695F70657266
+
+
+def key(r):
+    return (SEED ^ (r << 56)) & 0xFFFFFFFFFFFFFFFF
+
+
+def run(world, scenario, tmp_path):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    ps = [subprocess.Popen([sys.executable, os.path.join(HERE, "bench_dist_worker.py"), str(r), str(world), str(port),
+                            scenario, str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           env=env) for r in range(world)]
+    outs = [p.communicate(timeout=240)[0] for p in ps]
+    assert all(p.returncode == 0 for p in ps), [o[-800:] for o in outs]
+    return [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rounds_peers_and_expected_checksums(world, tmp_path):
+    res = run(world, "ok", tmp_path)
+    rounds = all_pairs_rounds(world)
+    n, iters, steps, warmup = 4096, 7, 5, 2
+    for d in res:
+        r = d["rank"]
+        assert d["engine_used"] == "kernel"
+        assert d["res"]["validated_rounds"] == world - 1
+        assert d["res"]["total"] == (world // 2) * n * iters * steps
+        imports = sorted(x[1] for x in d["log"] if x[0] == "import")
+        assert imports == [q for q in range(world) if q != r]
+        xf = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel"]
+        checked = [x for x in xf if x[8]]
+        timed = [x for x in xf if not x[8] and x[2] == 2]
+        # validation: one checked transfer per round, against the PEER's tx
+        assert len(checked) == world - 1
+        for rd, x in enumerate(checked):
+            g, peer = round_role(rounds, rd, r)
+            assert (x[3], x[4], x[5], x[6], x[7]) == (g, r, peer, 3, n)
+            assert x[9] == (key(peer) * 31 + n) & 0xFFFFFFFFFFFFFFFF
+            assert x[10] == (key(peer) * 31 + 1) & 0xFFFFFFFFFFFFFFFF
+        # warmup + timed steps: step s runs round s mod (N-1)
+        assert len(timed) == warmup + steps
+        for s, x in enumerate(timed):
+            g, peer = round_role(rounds, (s if s < warmup else s - warmup) % (world - 1), r)
+            assert (x[3], x[5], x[6], x[7]) == (g, peer, iters, n)
+    # every rank reports the same max-over-ranks elapsed time and per-launch time
+    assert len({d["res"]["elapsed"] for d in res}) == 1
+    assert len({d["res"]["per_launch_s"] for d in res}) == 1
+    # per_launch_s averages the G1 launches: G1 rank r reports 0.001*(1+r)
+    g1 = [round_role(rounds, s % (world - 1), r)[0] for r in range(world) for s in range(steps)]
+    assert sum(g1) == (world // 2) * steps
+    # the ping-pong latency probe ran on round 0 with 2000 iterations of 8 B
+    for d in res:
+        pp = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0]
+        assert len(pp) == 1 and pp[0][6] == 2000 and pp[0][7] == 8
+
+
+def test_error_on_one_rank_reaches_every_rank(tmp_path):
+    res = run(2, "import_fails", tmp_path)
+    for d in res:
+        # kernel engine fails on rank 1 -> every rank falls back; sdma fails too -> SystemExit on all
+        assert "rank 1" in d["exit"] and "cannot map rank 0" in d["exit"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_kernel_validation_failure_falls_back_to_sdma_with_a_label(world, tmp_path):
+    res = run(world, "kernel_fails_validation", tmp_path)
+    for d in res:
+        assert d["engine_used"].startswith("sdma (fallback")
+        assert "rank 0" in d["extras"]["kernel_engine_error"]
+        assert any(x[0] == "xfer" and x[1] == "sdma" and not x[8] for x in d["log"])
+        # the failed kernel context was closed before the SDMA one was opened
+        inits = [i for i, x in enumerate(d["log"]) if x[0] == "init"]
+        closes = [i for i, x in enumerate(d["log"]) if x[0] == "close" and x[1] == "kernel"]
+        assert closes and inits[1] > closes[0]
