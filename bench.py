@@ -38,6 +38,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
+from mpx.schedule import all_pairs_rounds, round_role  # noqa: E402  (pure Python, no GPU)
 
 HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # xGMI: BASELINE.json quotes ~153 GB/s per link.  That is the link's
@@ -129,14 +130,39 @@ def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: in
         return dict(median_s=statistics.median(res[1:]), per_iter_us=statistics.median(res[1:]) / iters * 1e6)
 
 
+def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes) -> dict:
+    """Diagnostics beside the headline: the pairs of round 0 at a few message
+    sizes (unidir, the reference's byte count B per iteration) and the -x 1
+    full-duplex loop at B (2B per iteration, mpi_perf.c:538).  Time = max over
+    ranks of the wall time of the loop; GB/s per pair."""
+    g, peer = round_role(rounds, 0, rank)
+    rates = {}
+
+    def timed(mode, n, it):
+        dist.barrier()
+        t = c.xfer(mode, g, rank, peer, it, tx, rx, n)
+        w = torch.tensor([t.wall_s], dtype=torch.float64)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        return float(w[0])
+
+    for n in sorted({8, 4096, 65536, 456131, nbytes}):
+        if n > nbytes:
+            continue
+        it = max(20, min(2000, (256 << 20) // n))
+        w = timed(mpx.MODE_UNIDIR, n, it)
+        rates[f"unidir_{n}"] = dict(us_per_iter=round(w / it * 1e6, 3), GBps=round(n * it / w / 1e9, 3))
+    it = max(20, min(500, (1 << 30) // nbytes))
+    w = timed(mpx.MODE_NONBLOCKING, nbytes, it)
+    rates[f"nonblocking_{nbytes}"] = dict(us_per_iter=round(w / it * 1e6, 3), GBps=round(2 * nbytes * it / w / 1e9, 3))
+    return rates
+
+
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
                 latency=True) -> dict:
     """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers).
     Every round's payloads are validated once (check mode, seeded per-rank
     patterns) before anything is timed.  Returns a dict; "error" is set (on
     every rank) if any rank failed."""
-    from mpx.schedule import all_pairs_rounds, round_role
-
     rounds = all_pairs_rounds(world)
     out = {}
     c = None
@@ -225,6 +251,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         lat = torch.tensor([lt.wall_s], dtype=torch.float64)
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
         out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / 4000 * 1e6, 3)
+        out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes)
     dist.barrier()
     c.close()
     dist.barrier()   # see above: all imports closed before the next allocation
@@ -353,6 +380,8 @@ def main() -> None:
         extras["per_pair_unidir_GBps"] = round(achieved, 2)
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
+        if "round0_sweep" in res:
+            extras["round0_sweep"] = res["round0_sweep"]
         if not args.no_extras:
             for eng in ("sdma", "rccl"):
                 if eng == engine_used:

@@ -54,7 +54,7 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         assert imports == [q for q in range(world) if q != r]
         xf = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel"]
         checked = [x for x in xf if x[8]]
-        timed = [x for x in xf if not x[8] and x[2] == 2]
+        timed = [x for x in xf if not x[8] and x[2] == 2][:warmup + steps]
         # validation: one checked transfer per round, against the PEER's tx
         assert len(checked) == world - 1
         for rd, x in enumerate(checked):
@@ -73,10 +73,17 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
     # per_launch_s averages the G1 launches: G1 rank r reports 0.001*(1+r)
     g1 = [round_role(rounds, s % (world - 1), r)[0] for r in range(world) for s in range(steps)]
     assert sum(g1) == (world // 2) * steps
-    # the ping-pong latency probe ran on round 0 with 2000 iterations of 8 B
+    # the ping-pong latency probe ran on round 0 with 2000 iterations of 8 B,
+    # then the round-0 size sweep (unidir) and the full-duplex -x 1 loop
     for d in res:
+        r = d["rank"]
         pp = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0]
         assert len(pp) == 1 and pp[0][6] == 2000 and pp[0][7] == 8
+        g, peer = round_role(rounds, 0, r)
+        sweep = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel" and not x[8]][warmup + steps + 1:]
+        assert [x[7] for x in sweep] == [8, n, n]            # sizes <= B (B = 4096 here), then -x 1 at B
+        assert [x[2] for x in sweep] == [2, 2, 1] and all((x[3], x[5]) == (g, peer) for x in sweep)
+        assert set(d["res"]["round0_sweep"]) == {"unidir_8", f"unidir_{n}", f"nonblocking_{n}"}
 
 
 def test_error_on_one_rank_reaches_every_rank(tmp_path):
