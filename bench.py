@@ -157,8 +157,42 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes) -> dict:
     return rates
 
 
+PUSH_WG_CANDIDATES = (16, 32, 64, 128, 256)
+
+
+def tune_push_wg_local(mpx, c, rounds, rank, tx, rx, nbytes, expect, expect_ack, iters=40) -> list[float]:
+    """Time round 0's unidir loop at B once per candidate bulk push width
+    (workgroups per push, mpx_xfer_opts.nwg), each width's payloads first
+    validated (check mode, 2 iterations).  No collectives: each pair
+    synchronises itself inside xfer, so a failure on one rank cannot leave
+    the others inside a collective.  Returns this rank's wall times
+    (0.0 for a width that does not apply)."""
+    g, peer = round_role(rounds, 0, rank)
+    times = []
+    for nwg in PUSH_WG_CANDIDATES:
+        if nbytes <= 8192 or nwg * 16 > nbytes:
+            times.append(0.0)
+            continue
+        c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 2, tx, rx, nbytes, check_payload=True, expect=expect[peer],
+               expect_ack=expect_ack[peer], timeout_ms=10000, nwg=nwg)
+        times.append(c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg).wall_s)
+    return times
+
+
+def pick_push_wg(torch, dist, times: list[float], nbytes: int, iters: int = 40) -> tuple[int, dict]:
+    """Max over ranks of every candidate's time; every rank then picks the
+    same width (the reduced tensor is identical everywhere)."""
+    w = torch.tensor(times, dtype=torch.float64)
+    dist.all_reduce(w, op=dist.ReduceOp.MAX)
+    rates = {nwg: nbytes * iters / float(t) / 1e9 for nwg, t in zip(PUSH_WG_CANDIDATES, w.tolist()) if t > 0}
+    if not rates:
+        return 0, {}
+    best = max(rates, key=rates.get)
+    return best, {str(k): round(v, 2) for k, v in rates.items()}
+
+
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                latency=True) -> dict:
+                latency=True, tune=True) -> dict:
     """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers).
     Every round's payloads are validated once (check mode, seeded per-rank
     patterns) before anything is timed.  Returns a dict; "error" is set (on
@@ -174,7 +208,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         return next((f for f in flags if f), "")
 
     # phase 1: local setup (no collectives inside the try)
-    mine, err = None, ""
+    mine, err, tune_times = None, "", None
     try:
         c = mpx.Context(world, engine)
         tx, rx = c.alloc(dev, nbytes), c.alloc(dev, nbytes)
@@ -203,6 +237,9 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
                 g, peer = round_role(rounds, r, rank)
                 c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True,
                        expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000)
+            if engine == "kernel" and tune:
+                tune_times = tune_push_wg_local(mpx, c, rounds, rank, tx, rx, nbytes, [d[1] for d in descs],
+                                                [d[2] for d in descs])
         except Exception as e:  # noqa: BLE001
             err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
         err = agree(err)
@@ -218,11 +255,15 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         dist.barrier()
         return {"error": err}
     out["validated_rounds"] = len(rounds)
+    nwg = 0
+    if tune_times is not None:
+        nwg, out["push_wg_tune"] = pick_push_wg(torch, dist, tune_times, nbytes)
+    out["push_wg"] = nwg
 
     def step(s: int):
         g, peer = round_role(rounds, s % len(rounds), rank)
         dist.barrier()                               # MPI_Barrier, mpi_perf.c:499
-        return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes)
+        return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg)
 
     for s in range(warmup):
         step(s)
@@ -376,7 +417,9 @@ def main() -> None:
                     avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
         config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=engine_used,
                       rounds=world - 1, pairs_per_round=world // 2, parallelism=f"pairs{world // 2}",
-                      validated_rounds=res["validated_rounds"])
+                      validated_rounds=res["validated_rounds"], push_workgroups=res.get("push_wg") or "default")
+        if res.get("push_wg_tune"):
+            extras["push_wg_tune_GBps_per_pair"] = res["push_wg_tune"]
         extras["per_pair_unidir_GBps"] = round(achieved, 2)
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]

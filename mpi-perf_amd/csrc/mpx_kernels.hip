@@ -26,6 +26,9 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 constexpr u64 kGolden = 0x9E3779B97F4A7C15ull;
 constexpr int kAuxSys = 17;                 // buffer cache policy: sc0 | sc1
+constexpr int kAuxSysVol = (int)0x80000011u; // sc0 | sc1, volatile (re-issued every poll)
+constexpr int kLLUnits = kLLGranules / 2;    // 16-B LL units (two granules each)
+constexpr int kLLUnitsPerLane = kLLUnits / kBlock;
 constexpr unsigned kRsrcWord3 = 0x00020000; // raw buffer, 32-bit data format
 
 __device__ __forceinline__ u64 mix64(u64 z) {
@@ -188,6 +191,26 @@ struct Loop {
     const XferArgs& a;
     int* s_abort;      // LDS: this workgroup gave up
     u64* lds4;         // LDS scratch for block_sum
+    // LL payload of this side's sends, held in VGPRs for the whole launch:
+    // pre[j] = tx bytes [8u, 8u+8) of unit u = threadIdx.x + j*kBlock.  tx is
+    // read-only while the loop runs (the reference re-sends the same buffer
+    // every iteration, mpi_perf.c:72,80,135), so a send is stores only — no
+    // tx load on the latency path.
+    u64 pre[kLLUnitsPerLane];
+
+    __device__ void preload_ll(long long n) {
+#pragma unroll
+        for (int j = 0; j < kLLUnitsPerLane; ++j) {
+            const long long off = 8ll * ((int)threadIdx.x + j * kBlock);
+            u64 w = 0;
+            if (off + 8 <= n) {
+                w = *reinterpret_cast<const u64*>(a.tx + off);
+            } else {
+                for (long long b = 0; off + b < n; ++b) w |= (u64)a.tx[off + b] << (8 * b);
+            }
+            pre[j] = w;
+        }
+    }
 
     __device__ bool aborted() const { return *s_abort != 0; }
 
@@ -229,17 +252,13 @@ struct Loop {
             return;
         }
         const __amdgpu_buffer_rsrc_t dst = rsrc(&a.peer_mb->ll[a.my_slot][0], (unsigned)(nu * 16));
-        for (int u = threadIdx.x; u < nu; u += kBlock) {
-            const long long off = 8ll * u;
-            u64 w;
-            if (off + 8 <= n) {
-                w = *reinterpret_cast<const u64*>(a.tx + off);
-            } else {
-                w = 0;
-                for (long long b = 0; off + b < n; ++b) w |= (u64)a.tx[off + b] << (8 * b);
+#pragma unroll
+        for (int j = 0; j < kLLUnitsPerLane; ++j) {
+            const int u = (int)threadIdx.x + j * kBlock;
+            if (u < nu) {
+                const v4u v = {(unsigned)pre[j], tag, (unsigned)(pre[j] >> 32), tag};
+                __builtin_amdgcn_raw_buffer_store_b128(v, dst, (unsigned)u * 16, 0, kAuxSys);
             }
-            const v4u v = {(unsigned)w, tag, (unsigned)(w >> 32), tag};
-            __builtin_amdgcn_raw_buffer_store_b128(v, dst, (unsigned)u * 16, 0, kAuxSys);
         }
     }
 
@@ -279,10 +298,57 @@ struct Loop {
     }
 
     // ---- receive: wait until the peer's push `seq` of n bytes has landed ----
-    // LL receive: every lane issues the loads of ALL its granules (up to 8)
+    // LL receive: every lane issues the loads of ALL its units (up to 4)
     // back to back, then checks the tags — one memory round trip per poll,
-    // not one per granule.
+    // not one per unit.
+    // 16-B form (ll_flags bit 0, default): one 16-B sc0|sc1 volatile load
+    // per unit, both granule tags checked (the sender tags both halves of
+    // every unit).  Against 8-B granule loads it halves the load count:
+    // 4 KiB ping-pong 4.32 -> 2.56 us per iteration (profiles/r01_ll_preload_ab.jsonl).
+    __device__ bool wait_ll16(long long n, u64 seq, int iter) const {
+        const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;
+        const int nu = (ng + 1) >> 1;
+        const int mine = nu > (int)threadIdx.x ? (nu - (int)threadIdx.x + kBlock - 1) / kBlock : 0;
+        const unsigned tag = ll_tag(seq);
+        const __amdgpu_buffer_rsrc_t src = rsrc(&a.my_mb->ll[a.peer_slot][0], (unsigned)(nu * 16));
+        v4u x[kLLUnitsPerLane];
+        if (mine > 0) {
+            const u64 t0 = now_ticks();
+            u64 spins = 0;
+            for (;;) {
+#pragma unroll
+                for (int j = 0; j < kLLUnitsPerLane; ++j)
+                    if (j < mine)
+                        x[j] = __builtin_amdgcn_raw_buffer_load_b128(src, ((unsigned)threadIdx.x + j * kBlock) * 16, 0,
+                                                                     kAuxSysVol);
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < kLLUnitsPerLane; ++j)
+                    if (j < mine) ok &= (x[j].y == tag) & (x[j].w == tag);
+                if (ok) break;
+                if (should_stop(++spins, t0)) { give_up(iter); break; }
+                __builtin_amdgcn_s_sleep(0);
+            }
+            if (blockIdx.x == 0 && !*s_abort) {
+#pragma unroll
+                for (int j = 0; j < kLLUnitsPerLane; ++j) {
+                    if (j >= mine) break;
+                    const long long off = 8ll * ((int)threadIdx.x + j * kBlock);
+                    const u64 d = ((u64)x[j].z << 32) | x[j].x;
+                    if (off + 8 <= n) {
+                        *reinterpret_cast<u64*>(a.rx + off) = d;
+                    } else {
+                        for (long long b = 0; off + b < n; ++b) a.rx[off + b] = (unsigned char)(d >> (8 * b));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
+
     __device__ bool wait_ll(long long n, u64 seq, int iter) const {
+        if ((a.ll_flags & 3) == 1) return wait_ll16(n, seq, iter);
         constexpr int kPer = kLLGranules / kBlock;         // granules per lane, max
         const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;
         const int mine = ng > (int)threadIdx.x ? (ng - (int)threadIdx.x + kBlock - 1) / kBlock : 0;
@@ -444,29 +510,38 @@ __global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
     __shared__ u64 lds4[4];
     if (threadIdx.x == 0) s_abort = 0;
     __syncthreads();
-    Loop L{a, &s_abort, lds4};
+    Loop L{a, &s_abort, lds4, {}};
     const long long n = a.len;
+    // the size this side sends: B, or the 1-byte ack of unidir group 0
+    const long long send_len = (a.mode == MPX_MODE_UNIDIR && a.group == 0) ? 1 : n;
+    const bool ll_send = blockIdx.x == 0 && (a.ll_flags & 1) && L.is_ll(send_len);
+    if (ll_send) L.preload_ll(send_len);
+    const bool reload = ll_send && (a.ll_flags & 4);   // A/B knob (bit 2): re-read tx at every send
     u64 txs = a.tx_seq0, rxs = a.rx_seq0;
     int inflight = 0;
     for (int i = 0; i < a.iters; ++i) {
         if (a.mode == MPX_MODE_PINGPONG) {            // mpi_perf.c:70-82
             if (a.group == 1) {
+                if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs);                      // Send(tx, B, tag 1)
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 2)
                 if (a.check) L.check(n, i);
             } else {
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 1)
                 if (a.check) L.check(n, i);
+                if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs);                      // Send(tx, B, tag 2)
             }
         } else if (a.mode == MPX_MODE_UNIDIR) {        // mpi_perf.c:132-144
             if (a.group == 1) {
+                if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs);                      // Send(tx, B)
                 if (!L.recv(1, ++rxs, i)) break;       // Recv(rx, 1) — the ack
                 if (a.check) L.check(1, i);
             } else {
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B)
                 if (a.check) { L.check(n, i); if (!L.grid_sync(i)) break; }
+                if (reload) L.preload_ll(send_len);
                 L.send(1, ++txs);                      // Send(tx, 1)
             }
         } else {                                       // mpi_perf.c:95-124

@@ -322,7 +322,14 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.group = group;
     a.my_slot = my_rank;
     a.peer_slot = peer_rank;
-    a.nwg = (o && o->nwg > 0) ? o->nwg : bulk_nwg(len, same_device(me, peer));
+    // push workgroups: the call's option, else MPX_PUSH_WG (every rank of a
+    // job inherits the same environment, so both sides agree), else the
+    // size rule bulk_nwg()
+    static const int env_nwg = [] {
+        const char* v = getenv("MPX_PUSH_WG");
+        return v ? atoi(v) : 0;
+    }();
+    a.nwg = (o && o->nwg > 0) ? o->nwg : env_nwg > 0 ? env_nwg : bulk_nwg(len, same_device(me, peer));
     if (a.nwg > kMaxPushWG) return fail(MPX_ERR_INVALID, "nwg %d > %d", a.nwg, kMaxPushWG);
     a.check = (o && o->check) ? 1 : 0;
     a.ll_flags = ll_flags();

@@ -82,12 +82,17 @@ class FakeMpx:
             FakeMpx.log.append(["rccl_init", r, n])
 
         def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,
-                 timeout_ms=0):
+                 timeout_ms=0, nwg=0):
             if check_payload and self.engine == "kernel" and scenario == "kernel_fails_validation" and rank == 0:
                 raise FakeError("payload checksum mismatch")
             FakeMpx.log.append(["xfer", self.engine, mode, group, me, peer, iters, n, bool(check_payload), expect,
-                                expect_ack])
+                                expect_ack, nwg])
             time.sleep(0.002)
+            if nwg and not check_payload:
+                # push-width tuning: rank 0 is fastest at 32, rank 1 slow at 32;
+                # the max over ranks is fastest at 64
+                ms = {16: 5, 32: 2 if rank != 1 else 7, 64: 3, 128: 4, 256: 6}[nwg]
+                return Timing(ms * 1e-3, ms * 1e-3)
             return Timing(0.002, 0.001 * (1 + me))
 
         def close(self):
@@ -98,7 +103,8 @@ dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank
 extras = {}
 out = {"rank": rank}
 try:
-    res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, 4096, 7, 5, 2,
+    nbytes = 65536 if scenario == "tune" else 4096
+    res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, nbytes, 7, 5, 2,
                                           dist.barrier, extras)
     out.update(res=res, engine_used=used, extras=extras)
 except SystemExit as e:
