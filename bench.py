@@ -130,11 +130,17 @@ def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: in
         return dict(median_s=statistics.median(res[1:]), per_iter_us=statistics.median(res[1:]) / iters * 1e6)
 
 
+# BASELINE config 3 / SURVEY §8d cfg3: the pair sweep uses config 1's sizes
+# (the reference's own CPU sweep) plus the reference's default B = 456131
+CFG3_SIZES = (1, 8, 64, 512, 4096, 32768, 262144, 456131, 1 << 20, 4 << 20)
+LATENCY_ITERS = 100_000     # cfg3: 8 B latency with I >= 10^5
+
+
 def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes) -> dict:
-    """Diagnostics beside the headline: the pairs of round 0 at a few message
-    sizes (unidir, the reference's byte count B per iteration) and the -x 1
-    full-duplex loop at B (2B per iteration, mpi_perf.c:538).  Time = max over
-    ranks of the wall time of the loop; GB/s per pair."""
+    """Config 3 beside the headline: the pairs of round 0 at every cfg3 size
+    <= B, unidirectional (`-u 1`, B per iteration) and bidirectional (`-x 1`
+    full duplex, 2B per iteration, mpi_perf.c:538).  Time = max over ranks of
+    the loop's wall time; GB/s per pair."""
     g, peer = round_role(rounds, 0, rank)
     rates = {}
 
@@ -145,15 +151,12 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes) -> dict:
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         return float(w[0])
 
-    for n in sorted({8, 4096, 65536, 456131, nbytes}):
-        if n > nbytes:
-            continue
+    for n in sorted(set(x for x in CFG3_SIZES if x <= nbytes) | {nbytes}):
         it = max(20, min(2000, (256 << 20) // n))
         w = timed(mpx.MODE_UNIDIR, n, it)
         rates[f"unidir_{n}"] = dict(us_per_iter=round(w / it * 1e6, 3), GBps=round(n * it / w / 1e9, 3))
-    it = max(20, min(500, (1 << 30) // nbytes))
-    w = timed(mpx.MODE_NONBLOCKING, nbytes, it)
-    rates[f"nonblocking_{nbytes}"] = dict(us_per_iter=round(w / it * 1e6, 3), GBps=round(2 * nbytes * it / w / 1e9, 3))
+        w = timed(mpx.MODE_NONBLOCKING, n, it)
+        rates[f"nonblocking_{n}"] = dict(us_per_iter=round(w / it * 1e6, 3), GBps=round(2 * n * it / w / 1e9, 3))
     return rates
 
 
@@ -288,10 +291,10 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     if latency:
         g, peer = round_role(rounds, 0, rank)
         dist.barrier()
-        lt = c.xfer(mpx.MODE_PINGPONG, g, rank, peer, 2000, tx, rx, 8)
+        lt = c.xfer(mpx.MODE_PINGPONG, g, rank, peer, LATENCY_ITERS, tx, rx, 8)
         lat = torch.tensor([lt.wall_s], dtype=torch.float64)
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
-        out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / 4000 * 1e6, 3)
+        out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / (2 * LATENCY_ITERS) * 1e6, 3)
         out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes)
     dist.barrier()
     c.close()

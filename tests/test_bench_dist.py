@@ -73,17 +73,19 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
     # per_launch_s averages the G1 launches: G1 rank r reports 0.001*(1+r)
     g1 = [round_role(rounds, s % (world - 1), r)[0] for r in range(world) for s in range(steps)]
     assert sum(g1) == (world // 2) * steps
-    # the ping-pong latency probe ran on round 0 with 2000 iterations of 8 B,
-    # then the round-0 size sweep (unidir) and the full-duplex -x 1 loop
+    # the ping-pong latency probe ran on round 0 with 10^5 iterations of 8 B,
+    # then the round-0 size sweep (config 3: unidir and full-duplex -x 1)
     for d in res:
         r = d["rank"]
         pp = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0]
-        assert len(pp) == 1 and pp[0][6] == 2000 and pp[0][7] == 8
+        assert len(pp) == 1 and pp[0][6] == 100_000 and pp[0][7] == 8
         g, peer = round_role(rounds, 0, r)
         sweep = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel" and not x[8]][warmup + steps + 1:]
-        assert [x[7] for x in sweep] == [8, n, n]            # sizes <= B (B = 4096 here), then -x 1 at B
-        assert [x[2] for x in sweep] == [2, 2, 1] and all((x[3], x[5]) == (g, peer) for x in sweep)
-        assert set(d["res"]["round0_sweep"]) == {"unidir_8", f"unidir_{n}", f"nonblocking_{n}"}
+        sizes = [1, 8, 64, 512, 4096]                        # config 3's sizes <= B (B = 4096 here)
+        assert [x[7] for x in sweep] == [m for m in sizes for _ in (0, 1)]
+        assert [x[2] for x in sweep] == [2, 1] * len(sizes)  # -u 1 then -x 1 at every size
+        assert all((x[3], x[5]) == (g, peer) for x in sweep)
+        assert set(d["res"]["round0_sweep"]) == {f"{m}_{k}" for k in sizes for m in ("unidir", "nonblocking")}
 
 
 def test_error_on_one_rank_reaches_every_rank(tmp_path):
