@@ -16,6 +16,8 @@ constexpr int kMaxPushWG = 256;          // flag slots per (receiver, sender) li
 constexpr int kLLMaxBytes = 8192;        // messages <= this go as LL granules
 constexpr int kLLGranules = kLLMaxBytes / 4;   // 4 payload bytes per granule
 constexpr int kNbWindow = 256;           // MAX_REQ_NUM, mpi_perf.c:88
+constexpr int kStageMaxBytes = 60 << 10; // LDS-staged tx chunk per workgroup, max
+                                         // (under a 64 KiB per-workgroup LDS limit)
 
 // Protocol ids reported in mpx_timing.protocol
 enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4 };
@@ -68,6 +70,8 @@ struct XferArgs {
                                  //       register-held payload)
     int ll_max;                  // messages <= ll_max bytes use LL (<= kLLMaxBytes);
                                  // same on both sides of the link
+    int stage;                   // bytes of dynamic LDS holding this workgroup's
+                                 // chunk of tx (0: bulk pushes read tx from HBM)
 };
 
 // LL threshold of a link.  Within one GPU the bulk path's extra hop (payload

@@ -191,6 +191,7 @@ struct Loop {
     const XferArgs& a;
     int* s_abort;      // LDS: this workgroup gave up
     u64* lds4;         // LDS scratch for block_sum
+    v4u* s_tx;         // LDS: this workgroup's staged chunk of tx (a.stage)
     // LL payload of this side's sends, held in VGPRs for the whole launch:
     // pre[j] = tx bytes [8u, 8u+8) of unit u = threadIdx.x + j*kBlock.  tx is
     // read-only while the loop runs (the reference re-sends the same buffer
@@ -262,26 +263,51 @@ struct Loop {
         }
     }
 
+    // this workgroup's chunk [lo, hi) of a bulk push of n bytes
+    __device__ void chunk_of(long long n, long long* lo, long long* hi) const {
+        const long long chunk = (((n + a.nwg - 1) / a.nwg) + 15) & ~15ll;
+        *lo = (long long)blockIdx.x * chunk;
+        *hi = *lo + chunk < n ? *lo + chunk : n;
+    }
+
+    // LDS staging (a.stage): each pushing workgroup copies its chunk's 16-B
+    // units of tx into LDS once per launch; every push then reads LDS
+    // (ds_read_b128) instead of HBM/L2, so the per-iteration critical path
+    // is LDS -> remote store.  tx is read-only while the loop runs.
+    __device__ void stage_tx(long long n) const {
+        if ((int)blockIdx.x >= a.nwg) return;
+        long long lo, hi;
+        chunk_of(n, &lo, &hi);
+        if (lo >= hi) return;
+        const int nv = (int)((hi - lo) >> 4);
+        const v4u* src = reinterpret_cast<const v4u*>(a.tx + lo);
+        for (int v = threadIdx.x; v < nv; v += kBlock) s_tx[v] = src[v];
+    }
+
+    template <bool LDS>
+    __device__ __forceinline__ void push_units(const v4u* src, __amdgpu_buffer_rsrc_t dst, int nv) const {
+        int v = threadIdx.x;
+        for (; v + 3 * kBlock < nv; v += 4 * kBlock) {
+            const v4u r0 = src[v], r1 = src[v + kBlock], r2 = src[v + 2 * kBlock], r3 = src[v + 3 * kBlock];
+            __builtin_amdgcn_raw_buffer_store_b128(r0, dst, v * 16, 0, kAuxSys);
+            __builtin_amdgcn_raw_buffer_store_b128(r1, dst, (v + kBlock) * 16, 0, kAuxSys);
+            __builtin_amdgcn_raw_buffer_store_b128(r2, dst, (v + 2 * kBlock) * 16, 0, kAuxSys);
+            __builtin_amdgcn_raw_buffer_store_b128(r3, dst, (v + 3 * kBlock) * 16, 0, kAuxSys);
+        }
+        for (; v < nv; v += kBlock) __builtin_amdgcn_raw_buffer_store_b128(src[v], dst, v * 16, 0, kAuxSys);
+    }
+
     __device__ void push_bulk(long long n, u64 seq) const {
         const int w = blockIdx.x;
         if (w >= a.nwg) return;
-        const long long chunk = (((n + a.nwg - 1) / a.nwg) + 15) & ~15ll;
-        const long long lo = (long long)w * chunk;
-        const long long hi = lo + chunk < n ? lo + chunk : n;
+        long long lo, hi;
+        chunk_of(n, &lo, &hi);
         if (lo < hi) {
             const unsigned bytes = (unsigned)(hi - lo);
             const __amdgpu_buffer_rsrc_t dst = rsrc(a.peer_rx + lo, bytes);
-            const v4u* src = reinterpret_cast<const v4u*>(a.tx + lo);
             const int nv = (int)(bytes >> 4);
-            int v = threadIdx.x;
-            for (; v + 3 * kBlock < nv; v += 4 * kBlock) {
-                const v4u r0 = src[v], r1 = src[v + kBlock], r2 = src[v + 2 * kBlock], r3 = src[v + 3 * kBlock];
-                __builtin_amdgcn_raw_buffer_store_b128(r0, dst, v * 16, 0, kAuxSys);
-                __builtin_amdgcn_raw_buffer_store_b128(r1, dst, (v + kBlock) * 16, 0, kAuxSys);
-                __builtin_amdgcn_raw_buffer_store_b128(r2, dst, (v + 2 * kBlock) * 16, 0, kAuxSys);
-                __builtin_amdgcn_raw_buffer_store_b128(r3, dst, (v + 3 * kBlock) * 16, 0, kAuxSys);
-            }
-            for (; v < nv; v += kBlock) __builtin_amdgcn_raw_buffer_store_b128(src[v], dst, v * 16, 0, kAuxSys);
+            if (a.stage) push_units<true>(s_tx, dst, nv);
+            else push_units<false>(reinterpret_cast<const v4u*>(a.tx + lo), dst, nv);
             const unsigned tail = bytes & 15;
             if (threadIdx.x < tail) {
                 const unsigned o = (unsigned)nv * 16 + threadIdx.x;
@@ -508,10 +534,12 @@ struct Loop {
 __global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
     __shared__ int s_abort;
     __shared__ u64 lds4[4];
+    extern __shared__ v4u s_tx[];            // a.stage: dynamic LDS = one chunk
     if (threadIdx.x == 0) s_abort = 0;
-    __syncthreads();
-    Loop L{a, &s_abort, lds4, {}};
+    Loop L{a, &s_abort, lds4, s_tx, {}};
     const long long n = a.len;
+    if (a.stage) L.stage_tx(n);
+    __syncthreads();
     // the size this side sends: B, or the 1-byte ack of unidir group 0
     const long long send_len = (a.mode == MPX_MODE_UNIDIR && a.group == 0) ? 1 : n;
     const bool ll_send = blockIdx.x == 0 && (a.ll_flags & 1) && L.is_ll(send_len);
@@ -565,7 +593,7 @@ __global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
 // ---------------------------------------------------------------------------
 hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
-    hipLaunchKernelGGL(k_xfer, dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_xfer, dim3(grid), dim3(kBlock), (unsigned)a.stage, s, a);
     return hipGetLastError();
 }
 

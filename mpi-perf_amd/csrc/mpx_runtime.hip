@@ -340,6 +340,23 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     const bool pushes_len = mode != MPX_MODE_UNIDIR || group == 1;
     const bool recvs_len = mode != MPX_MODE_UNIDIR || group == 0;
     const int grid = (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;
+    // bulk pushes read tx from LDS when one workgroup's chunk fits
+    // (kStageMaxBytes); MPX_STAGE=0 turns it off (A/B)
+    static const bool stage_on = [] {
+        const char* v = getenv("MPX_STAGE");
+        return !(v && atoi(v) == 0);
+    }();
+    if (stage_on && !ll && pushes_len && len > 0) {
+        static const long long lds_cap = [] {
+            int dev = 0, per_block = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&per_block, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+                per_block = 0;
+            return (long long)per_block - 1024;   // room for k_xfer's static LDS
+        }();
+        const long long chunk = (((len + a.nwg - 1) / a.nwg) + 15) & ~15ll;
+        if (chunk <= kStageMaxBytes && chunk <= lds_cap) a.stage = (int)chunk;
+    }
 
     HIPCK(hipMemsetAsync(me.scratch, 0, 2 * sizeof(u64), me.stream));
     if (a.check) HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
