@@ -91,7 +91,7 @@ class Pairs:
         tx = self.bufs[self.peer(r)][0]
         return self.c.checksum(tx, n), self.c.checksum(tx, 1)
 
-    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None):
+    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0):
         ranks = list(range(2 * self.np)) if ranks is None else ranks
         exp = {r: self.expect(r, n) for r in ranks}
         out, errs = {}, {}
@@ -100,7 +100,7 @@ class Pairs:
             try:
                 out[r] = self.c.xfer(mode, self.group(r), r, self.peer(r), iters, self.bufs[r][0], self.bufs[r][1],
                                      n, check_payload=check, expect=exp[r][0], expect_ack=exp[r][1],
-                                     timeout_ms=timeout_ms)
+                                     timeout_ms=timeout_ms, nwg=nwg)
             except mpx.MpxError as e:
                 errs[r] = e
 
@@ -139,6 +139,34 @@ def test_loopback_pair_every_payload(engine, mode):
                 m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else n
                 want = P.c.checksum(P.bufs[P.peer(r)][0], m)
                 assert P.c.checksum(P.bufs[r][1], m) == want, (n, r)
+    finally:
+        P.close()
+
+
+# (push workgroups, B): chunk = ceil(B / nwg) rounded up to 16 B; chunks of
+# <= 60 KiB are pushed from LDS (stage_tx), larger ones straight from HBM
+PUSH_CASES = [(1, 40000), (1, 70001), (7, 456131), (8, 456131), (33, (1 << 20) + 17), (128, (4 << 20) + 3),
+              (256, (20 << 20) + 5)]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_push_widths_staged_and_unstaged(mode):
+    """Bulk pushes at explicit widths (mpx_xfer_opts.nwg, as bench.py's tuner
+    sets them), both sides of the 60 KiB LDS-staging limit, ragged sizes:
+    every payload checksummed, the final rx compared with the peer's tx."""
+    P = Pairs("kernel", 1, (20 << 20) + 5, fill="pattern")
+    try:
+        for nwg, n in PUSH_CASES:
+            out, errs = P.run(mode, n, 5, nwg=nwg)
+            assert not errs, (nwg, n, errs)
+            for r in (0, 1):
+                pushes = mode != mpx.MODE_UNIDIR or r == 0
+                if pushes:
+                    assert out[r].nwg == nwg and out[r].protocol == 1, (nwg, n, r)
+                if mode != mpx.MODE_NONBLOCKING:
+                    assert out[r].check_failures == 0 and out[r].check_iters == 5
+                m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else n
+                assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (nwg, n, r)
     finally:
         P.close()
 
