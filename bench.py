@@ -232,7 +232,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     if not err:
         try:
             for r in range(world):
-                if r != rank:
+                if r != rank and engine != "rccl":   # RCCL maps its own buffers
                     c.import_rank(r, descs[r][0])
             if engine == "rccl":
                 c.rccl_init_rank(rank, world, uid[0])
@@ -310,11 +310,20 @@ def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iter
     res = pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync)
     engine_used = engine
     if res.get("error") and engine == "kernel":
-        fb = pairs_bench(mpx, torch, dist, "sdma", rank, world, dev, nbytes, iters, steps, warmup, barrier_sync)
         extras["kernel_engine_error"] = res["error"]
-        res, engine_used = fb, "sdma (fallback: kernel engine failed validation)"
+        # SDMA needs the same IPC mappings as the kernel engine; RCCL maps its
+        # own buffers, so it is the last resort when IPC itself failed
+        for fb_engine in ("sdma", "rccl"):
+            fb = pairs_bench(mpx, torch, dist, fb_engine, rank, world, dev, nbytes, iters, steps, warmup,
+                             barrier_sync)
+            if not fb.get("error"):
+                res, engine_used = fb, f"{fb_engine} (fallback: kernel engine failed validation)"
+                break
+            extras[f"{fb_engine}_engine_error"] = fb["error"]
     if res.get("error"):
-        raise SystemExit(f"pairs bench failed: {res['error']}")
+        errs = [f"{engine}: {res['error']}"] + [f"{k[:-len('_engine_error')]}: {v}" for k, v in extras.items()
+                                               if k.endswith("_engine_error") and not k.startswith(engine)]
+        raise SystemExit("pairs bench failed: " + "; ".join(errs))
     return res, engine_used
 
 

@@ -900,10 +900,14 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     Rank& me = ctx->r[my_rank];
     Rank& peer = ctx->r[peer_rank];
     if (!me.local) return fail(MPX_ERR_STATE, "rank %d is not attached in this process", my_rank);
-    if (!peer.local && !peer.imported) return fail(MPX_ERR_STATE, "peer rank %d is unknown (attach or import it)", peer_rank);
+    // RCCL addresses the peer by its communicator rank and maps nothing itself;
+    // the kernel and SDMA engines write into the peer's rx and mailbox
+    const bool rccl = ctx->engine == MPX_ENGINE_RCCL;
+    if (!rccl && !peer.local && !peer.imported)
+        return fail(MPX_ERR_STATE, "peer rank %d is unknown (attach or import it)", peer_rank);
     if (me.broken) return fail(MPX_ERR_STATE, "rank %d: a previous transfer timed out", my_rank);
     if (tx != me.tx || rx != me.rx) return fail(MPX_ERR_INVALID, "tx/rx are not rank %d's attached buffers", my_rank);
-    if ((size_t)buff_len > me.len || (size_t)buff_len > peer.len)
+    if ((size_t)buff_len > me.len || (!rccl && (size_t)buff_len > peer.len))
         return fail(MPX_ERR_INVALID, "buff_len %d exceeds an attached length (%zu, %zu)", buff_len, me.len, peer.len);
     const int check = opts && opts->check;
     if (check) TRY(ensure_csum(me, iters));

@@ -72,13 +72,15 @@ class FakeMpx:
             return (self.filled * 31 + n) & 0xFFFFFFFFFFFFFFFF     # a function of this rank's tx
 
         def import_rank(self, r, desc):
-            if scenario == "import_fails" and rank == 1:
+            if scenario in ("import_fails", "all_fail") and rank == 1:
                 raise FakeError(f"cannot map rank {r}")
             assert desc == f"desc-of-{r}".encode(), (r, desc)
             FakeMpx.log.append(["import", r])
 
         def rccl_init_rank(self, r, n, uid):
             assert uid == b"uid-from-rank-0"
+            if scenario == "all_fail" and rank == 1:
+                raise FakeError("ncclCommInitRank failed")
             FakeMpx.log.append(["rccl_init", r, n])
 
         def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,

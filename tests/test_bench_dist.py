@@ -88,11 +88,26 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         assert set(d["res"]["round0_sweep"]) == {f"{m}_{k}" for k in sizes for m in ("unidir", "nonblocking")}
 
 
-def test_error_on_one_rank_reaches_every_rank(tmp_path):
+def test_ipc_failure_on_one_rank_falls_back_to_rccl_on_every_rank(tmp_path):
+    """IPC import fails on rank 1: the kernel and SDMA engines (which write
+    into IPC-mapped peer memory) fail on every rank; RCCL maps nothing of
+    ours and carries the bench, labelled."""
     res = run(2, "import_fails", tmp_path)
     for d in res:
-        # kernel engine fails on rank 1 -> every rank falls back; sdma fails too -> SystemExit on all
-        assert "rank 1" in d["exit"] and "cannot map rank 0" in d["exit"]
+        assert d["engine_used"].startswith("rccl (fallback")
+        for eng in ("kernel", "sdma"):
+            assert "rank 1" in d["extras"][f"{eng}_engine_error"] and "cannot map rank 0" in d["extras"][
+                f"{eng}_engine_error"]
+        assert not any(x[0] == "import" for x in d["log"][[x[0] for x in d["log"]].index("rccl_init"):])
+
+
+def test_error_on_one_rank_reaches_every_rank(tmp_path):
+    res = run(2, "all_fail", tmp_path)
+    for d in res:
+        # every engine fails on rank 1 -> SystemExit naming every engine's error on all ranks
+        assert d["exit"].startswith("pairs bench failed: kernel: rank 1")
+        assert "sdma: rank 1: FakeError: cannot map rank 0" in d["exit"]
+        assert "rccl: rank 1: FakeError: ncclCommInitRank failed" in d["exit"]
 
 
 @pytest.mark.parametrize("world", [2, 4])
