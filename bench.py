@@ -160,38 +160,46 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes) -> dict:
     return rates
 
 
-PUSH_WG_CANDIDATES = (16, 32, 64, 128, 256)
+# bulk push variants tuned on the node's own links: (workgroups per push,
+# streaming hint on the payload stores, mpx_xfer_opts.flags MPX_XFER_STREAM)
+PUSH_CANDIDATES = tuple((w, st) for w in (16, 32, 64, 128, 256) for st in (False, True))
+TUNE_ITERS = 40
 
 
-def tune_push_wg_local(mpx, c, rounds, rank, tx, rx, nbytes, expect, expect_ack, iters=40) -> list[float]:
-    """Time round 0's unidir loop at B once per candidate bulk push width
-    (workgroups per push, mpx_xfer_opts.nwg), each width's payloads first
-    validated (check mode, 2 iterations).  No collectives: each pair
-    synchronises itself inside xfer, so a failure on one rank cannot leave
-    the others inside a collective.  Returns this rank's wall times
-    (0.0 for a width that does not apply)."""
+def push_name(nwg: int, stream: bool) -> str:
+    return f"{nwg}{'+nt' if stream else ''}"
+
+
+def tune_push_local(mpx, c, rounds, rank, tx, rx, nbytes, expect, expect_ack) -> list[float]:
+    """Time round 0's unidir loop at B once per bulk push variant (width =
+    workgroups per push, mpx_xfer_opts.nwg; streaming store hint), each
+    variant's payloads first validated (check mode, 2 iterations).  No
+    collectives: each pair synchronises itself inside xfer, so a failure on
+    one rank cannot leave the others inside a collective.  Returns this
+    rank's wall times (0.0 for a variant that does not apply)."""
     g, peer = round_role(rounds, 0, rank)
     times = []
-    for nwg in PUSH_WG_CANDIDATES:
+    for nwg, stream in PUSH_CANDIDATES:
         if nbytes <= 8192 or nwg * 16 > nbytes:
             times.append(0.0)
             continue
         c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 2, tx, rx, nbytes, check_payload=True, expect=expect[peer],
-               expect_ack=expect_ack[peer], timeout_ms=10000, nwg=nwg)
-        times.append(c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg).wall_s)
+               expect_ack=expect_ack[peer], timeout_ms=10000, nwg=nwg, stream=stream)
+        times.append(c.xfer(mpx.MODE_UNIDIR, g, rank, peer, TUNE_ITERS, tx, rx, nbytes, nwg=nwg,
+                            stream=stream).wall_s)
     return times
 
 
-def pick_push_wg(torch, dist, times: list[float], nbytes: int, iters: int = 40) -> tuple[int, dict]:
-    """Max over ranks of every candidate's time; every rank then picks the
-    same width (the reduced tensor is identical everywhere)."""
+def pick_push(torch, dist, times: list[float], nbytes: int) -> tuple[tuple[int, bool], dict]:
+    """Max over ranks of every variant's time; every rank then picks the
+    same variant (the reduced tensor is identical everywhere)."""
     w = torch.tensor(times, dtype=torch.float64)
     dist.all_reduce(w, op=dist.ReduceOp.MAX)
-    rates = {nwg: nbytes * iters / float(t) / 1e9 for nwg, t in zip(PUSH_WG_CANDIDATES, w.tolist()) if t > 0}
+    rates = {cand: nbytes * TUNE_ITERS / float(t) / 1e9 for cand, t in zip(PUSH_CANDIDATES, w.tolist()) if t > 0}
     if not rates:
-        return 0, {}
+        return (0, False), {}
     best = max(rates, key=rates.get)
-    return best, {str(k): round(v, 2) for k, v in rates.items()}
+    return best, {push_name(*k): round(v, 2) for k, v in rates.items()}
 
 
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
@@ -241,8 +249,8 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
                 c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True,
                        expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000)
             if engine == "kernel" and tune:
-                tune_times = tune_push_wg_local(mpx, c, rounds, rank, tx, rx, nbytes, [d[1] for d in descs],
-                                                [d[2] for d in descs])
+                tune_times = tune_push_local(mpx, c, rounds, rank, tx, rx, nbytes, [d[1] for d in descs],
+                                             [d[2] for d in descs])
         except Exception as e:  # noqa: BLE001
             err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
         err = agree(err)
@@ -258,15 +266,15 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         dist.barrier()
         return {"error": err}
     out["validated_rounds"] = len(rounds)
-    nwg = 0
+    nwg, stream = 0, False
     if tune_times is not None:
-        nwg, out["push_wg_tune"] = pick_push_wg(torch, dist, tune_times, nbytes)
-    out["push_wg"] = nwg
+        (nwg, stream), out["push_tune"] = pick_push(torch, dist, tune_times, nbytes)
+    out["push"] = push_name(nwg, stream) if nwg else "default"
 
     def step(s: int):
         g, peer = round_role(rounds, s % len(rounds), rank)
         dist.barrier()                               # MPI_Barrier, mpi_perf.c:499
-        return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg)
+        return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream)
 
     for s in range(warmup):
         step(s)
@@ -429,9 +437,9 @@ def main() -> None:
                     avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
         config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=engine_used,
                       rounds=world - 1, pairs_per_round=world // 2, parallelism=f"pairs{world // 2}",
-                      validated_rounds=res["validated_rounds"], push_workgroups=res.get("push_wg") or "default")
-        if res.get("push_wg_tune"):
-            extras["push_wg_tune_GBps_per_pair"] = res["push_wg_tune"]
+                      validated_rounds=res["validated_rounds"], push=res.get("push", "default"))
+        if res.get("push_tune"):
+            extras["push_tune_GBps_per_pair"] = res["push_tune"]
         extras["per_pair_unidir_GBps"] = round(achieved, 2)
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]

@@ -108,7 +108,7 @@ typedef struct mpx_timing {
 /* options of mpx_xfer_ex beyond the reference seam */
 typedef struct mpx_xfer_opts {
     int32_t check;            /* 1: checksum + poison every received payload   */
-    int32_t reserved0;
+    int32_t flags;            /* MPX_XFER_* bits below; 0 = defaults            */
     uint64_t expect_checksum; /* mpx_checksum() of the peer's tx[0:len) (B-byte
                                  receives) — required when check = 1           */
     uint64_t expect_ack;      /* mpx_checksum() of the peer's tx[0:1) (unidir
@@ -116,6 +116,11 @@ typedef struct mpx_xfer_opts {
     uint32_t timeout_ms;      /* per-wait device deadline; 0 = default (10 s)  */
     int32_t nwg;              /* override push workgroups; 0 = automatic        */
 } mpx_xfer_opts;
+
+/* mpx_xfer_opts.flags: bulk payload stores carry the streaming (nontemporal)
+   hint on top of their system-scope write-through policy (sc0 sc1 nt instead
+   of sc0 sc1).  Visibility is unchanged, so the two sides need not agree. */
+#define MPX_XFER_STREAM 1
 
 /* opaque context */
 typedef struct mpx_ctx mpx_ctx;

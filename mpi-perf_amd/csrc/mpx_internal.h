@@ -70,6 +70,7 @@ struct XferArgs {
                                  //       register-held payload)
     int ll_max;                  // messages <= ll_max bytes use LL (<= kLLMaxBytes);
                                  // same on both sides of the link
+    int stream;                  // 1: bulk payload stores add the nt hint (sc0 sc1 nt)
     int stage;                   // bytes of dynamic LDS holding this workgroup's
                                  // chunk of tx (0: bulk pushes read tx from HBM)
 };

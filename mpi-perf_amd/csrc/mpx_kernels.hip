@@ -26,6 +26,7 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 constexpr u64 kGolden = 0x9E3779B97F4A7C15ull;
 constexpr int kAuxSys = 17;                 // buffer cache policy: sc0 | sc1
+constexpr int kAuxSysNt = 19;               // sc0 | nt | sc1 (MPX_XFER_STREAM)
 constexpr int kAuxSysVol = (int)0x80000011u; // sc0 | sc1, volatile (re-issued every poll)
 constexpr int kLLUnits = kLLGranules / 2;    // 16-B LL units (two granules each)
 constexpr int kLLUnitsPerLane = kLLUnits / kBlock;
@@ -284,17 +285,17 @@ struct Loop {
         for (int v = threadIdx.x; v < nv; v += kBlock) s_tx[v] = src[v];
     }
 
-    template <bool LDS>
+    template <int AUX>
     __device__ __forceinline__ void push_units(const v4u* src, __amdgpu_buffer_rsrc_t dst, int nv) const {
         int v = threadIdx.x;
         for (; v + 3 * kBlock < nv; v += 4 * kBlock) {
             const v4u r0 = src[v], r1 = src[v + kBlock], r2 = src[v + 2 * kBlock], r3 = src[v + 3 * kBlock];
-            __builtin_amdgcn_raw_buffer_store_b128(r0, dst, v * 16, 0, kAuxSys);
-            __builtin_amdgcn_raw_buffer_store_b128(r1, dst, (v + kBlock) * 16, 0, kAuxSys);
-            __builtin_amdgcn_raw_buffer_store_b128(r2, dst, (v + 2 * kBlock) * 16, 0, kAuxSys);
-            __builtin_amdgcn_raw_buffer_store_b128(r3, dst, (v + 3 * kBlock) * 16, 0, kAuxSys);
+            __builtin_amdgcn_raw_buffer_store_b128(r0, dst, v * 16, 0, AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(r1, dst, (v + kBlock) * 16, 0, AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(r2, dst, (v + 2 * kBlock) * 16, 0, AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(r3, dst, (v + 3 * kBlock) * 16, 0, AUX);
         }
-        for (; v < nv; v += kBlock) __builtin_amdgcn_raw_buffer_store_b128(src[v], dst, v * 16, 0, kAuxSys);
+        for (; v < nv; v += kBlock) __builtin_amdgcn_raw_buffer_store_b128(src[v], dst, v * 16, 0, AUX);
     }
 
     __device__ void push_bulk(long long n, u64 seq) const {
@@ -306,8 +307,9 @@ struct Loop {
             const unsigned bytes = (unsigned)(hi - lo);
             const __amdgpu_buffer_rsrc_t dst = rsrc(a.peer_rx + lo, bytes);
             const int nv = (int)(bytes >> 4);
-            if (a.stage) push_units<true>(s_tx, dst, nv);
-            else push_units<false>(reinterpret_cast<const v4u*>(a.tx + lo), dst, nv);
+            const v4u* src = a.stage ? s_tx : reinterpret_cast<const v4u*>(a.tx + lo);
+            if (a.stream) push_units<kAuxSysNt>(src, dst, nv);
+            else push_units<kAuxSys>(src, dst, nv);
             const unsigned tail = bytes & 15;
             if (threadIdx.x < tail) {
                 const unsigned o = (unsigned)nv * 16 + threadIdx.x;

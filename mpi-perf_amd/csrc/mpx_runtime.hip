@@ -332,6 +332,11 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.nwg = (o && o->nwg > 0) ? o->nwg : env_nwg > 0 ? env_nwg : bulk_nwg(len, same_device(me, peer));
     if (a.nwg > kMaxPushWG) return fail(MPX_ERR_INVALID, "nwg %d > %d", a.nwg, kMaxPushWG);
     a.check = (o && o->check) ? 1 : 0;
+    static const bool env_stream = [] {
+        const char* v = getenv("MPX_PUSH_STREAM");
+        return v && atoi(v) != 0;
+    }();
+    a.stream = ((o && (o->flags & MPX_XFER_STREAM)) || env_stream) ? 1 : 0;
     a.ll_flags = ll_flags();
     a.ll_max = ll_max_bytes(same_device(me, peer));
     if (const char* v = getenv("MPX_LL_MAX")) a.ll_max = atoi(v) < kLLMaxBytes ? atoi(v) : kLLMaxBytes;

@@ -26,6 +26,7 @@ ENGINES = {"kernel": ENGINE_KERNEL, "sdma": ENGINE_SDMA, "rccl": ENGINE_RCCL}
 MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
 MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": MODE_UNIDIR}
 FILL_BYTE, FILL_SPLITMIX = 0, 1
+XFER_STREAM = 1
 PATTERN_SEED = 0x6D70695F70657266
 MAX_RANKS = 16
 RANK_DESC_BYTES = 512
@@ -54,7 +55,7 @@ class Timing(C.Structure):
 class XferOpts(C.Structure):
     _fields_ = [
         ("check", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("flags", C.c_int32),
         ("expect_checksum", C.c_uint64),
         ("expect_ack", C.c_uint64),
         ("timeout_ms", C.c_uint32),
@@ -202,9 +203,9 @@ class Context:
 
     def xfer(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, tx: Buffer, rx: Buffer,
              length: int, check_payload: bool = False, expect: int = 0, expect_ack: int = 0,
-             timeout_ms: int = 0, nwg: int = 0) -> Timing:
-        o = XferOpts(check=1 if check_payload else 0, expect_checksum=expect, expect_ack=expect_ack,
-                     timeout_ms=timeout_ms, nwg=nwg)
+             timeout_ms: int = 0, nwg: int = 0, stream: bool = False) -> Timing:
+        o = XferOpts(check=1 if check_payload else 0, flags=XFER_STREAM if stream else 0, expect_checksum=expect,
+                     expect_ack=expect_ack, timeout_ms=timeout_ms, nwg=nwg)
         t = Timing()
         st = self.L.mpx_xfer_ex(self.h, mode, group, my_rank, peer_rank, iters, C.c_void_p(tx.ptr),
                                 C.c_void_p(rx.ptr), length, C.byref(o), C.byref(t))

@@ -84,16 +84,17 @@ class FakeMpx:
             FakeMpx.log.append(["rccl_init", r, n])
 
         def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,
-                 timeout_ms=0, nwg=0):
+                 timeout_ms=0, nwg=0, stream=False):
             if check_payload and self.engine == "kernel" and scenario == "kernel_fails_validation" and rank == 0:
                 raise FakeError("payload checksum mismatch")
             FakeMpx.log.append(["xfer", self.engine, mode, group, me, peer, iters, n, bool(check_payload), expect,
-                                expect_ack, nwg])
+                                expect_ack, nwg, stream])
             time.sleep(0.002)
-            if nwg and not check_payload:
-                # push-width tuning: rank 0 is fastest at 32, rank 1 slow at 32;
-                # the max over ranks is fastest at 64
-                ms = {16: 5, 32: 2 if rank != 1 else 7, 64: 3, 128: 4, 256: 6}[nwg]
+            if nwg and not check_payload and iters == 40:
+                # push tuning: rank 0 is fastest at 32, rank 1 slow at 32; the
+                # max over ranks is fastest at 64 with the streaming hint
+                ms = {16: 5, 32: 2 if rank != 1 else 7, 64: 3, 128: 4, 256: 6}[nwg] + (0 if stream and nwg == 64
+                                                                                       else 0.5)
                 return Timing(ms * 1e-3, ms * 1e-3)
             return Timing(0.002, 0.001 * (1 + me))
 

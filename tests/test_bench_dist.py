@@ -124,25 +124,32 @@ def test_kernel_validation_failure_falls_back_to_sdma_with_a_label(world, tmp_pa
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_push_width_tuning_agrees_across_ranks(world, tmp_path):
-    """B > the LL landing zone: every candidate push width is validated
-    (check mode, the peer's checksums) and timed on round 0; the max over
-    ranks picks one width for every rank, and every timed step uses it."""
+def test_push_tuning_agrees_across_ranks(world, tmp_path):
+    """B > the LL landing zone: every push variant (width x streaming hint) is
+    validated (check mode, the peer's checksums) and timed on round 0; the
+    max over ranks picks one variant for every rank, and every timed step
+    uses it."""
     res = run(world, "tune", tmp_path)
     rounds = all_pairs_rounds(world)
     n, warmup, steps = 65536, 2, 5
+    ms = {16: 5, 32: 7, 64: 3, 128: 4, 256: 6}
+    want = {}
+    for w in (16, 32, 64, 128, 256):
+        for st in (False, True):
+            t = ms[w] + (0 if st and w == 64 else 0.5)
+            want[f"{w}{'+nt' if st else ''}"] = round(n * 40 / (t * 1e-3) / 1e9, 2)
     for d in res:
         r = d["rank"]
         g, peer = round_role(rounds, 0, r)
-        assert d["res"]["push_wg"] == 64
-        assert d["res"]["push_wg_tune"] == {str(w): round(n * 40 / (ms * 1e-3) / 1e9, 2) for w, ms in
-                                            {16: 5, 32: 7, 64: 3, 128: 4, 256: 6}.items()}
+        assert d["res"]["push"] == "64+nt"
+        assert d["res"]["push_tune"] == want
         xf = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel"]
         tuned = [x for x in xf if x[11]][:20]
-        for i, w in enumerate((16, 32, 64, 128, 256)):
+        cands = [(w, st) for w in (16, 32, 64, 128, 256) for st in (False, True)]
+        for i, (w, st) in enumerate(cands):
             chk, timed = tuned[2 * i], tuned[2 * i + 1]
-            assert chk[8] and chk[11] == w and (chk[3], chk[5]) == (g, peer)
+            assert chk[8] and chk[11] == w and chk[12] == st and (chk[3], chk[5]) == (g, peer)
             assert chk[9] == (key(peer) * 31 + n) & 0xFFFFFFFFFFFFFFFF
-            assert not timed[8] and timed[11] == w and timed[6] == 40
+            assert not timed[8] and timed[11] == w and timed[12] == st and timed[6] == 40
         steps_run = [x for x in xf if not x[8] and x[2] == 2 and x[6] == 7]
-        assert len(steps_run) == warmup + steps and all(x[11] == 64 for x in steps_run)
+        assert len(steps_run) == warmup + steps and all(x[11] == 64 and x[12] for x in steps_run)

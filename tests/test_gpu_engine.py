@@ -91,7 +91,7 @@ class Pairs:
         tx = self.bufs[self.peer(r)][0]
         return self.c.checksum(tx, n), self.c.checksum(tx, 1)
 
-    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0):
+    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0, stream=False):
         ranks = list(range(2 * self.np)) if ranks is None else ranks
         exp = {r: self.expect(r, n) for r in ranks}
         out, errs = {}, {}
@@ -100,7 +100,7 @@ class Pairs:
             try:
                 out[r] = self.c.xfer(mode, self.group(r), r, self.peer(r), iters, self.bufs[r][0], self.bufs[r][1],
                                      n, check_payload=check, expect=exp[r][0], expect_ack=exp[r][1],
-                                     timeout_ms=timeout_ms, nwg=nwg)
+                                     timeout_ms=timeout_ms, nwg=nwg, stream=stream)
             except mpx.MpxError as e:
                 errs[r] = e
 
@@ -149,15 +149,17 @@ PUSH_CASES = [(1, 40000), (1, 70001), (7, 456131), (8, 456131), (33, (1 << 20) +
               (256, (20 << 20) + 5)]
 
 
+@pytest.mark.parametrize("stream", [False, True])
 @pytest.mark.parametrize("mode", MODES)
-def test_push_widths_staged_and_unstaged(mode):
+def test_push_widths_staged_and_unstaged(mode, stream):
     """Bulk pushes at explicit widths (mpx_xfer_opts.nwg, as bench.py's tuner
-    sets them), both sides of the 60 KiB LDS-staging limit, ragged sizes:
-    every payload checksummed, the final rx compared with the peer's tx."""
+    sets them), with and without the streaming store hint, both sides of the
+    60 KiB LDS-staging limit, ragged sizes: every payload checksummed, the
+    final rx compared with the peer's tx."""
     P = Pairs("kernel", 1, (20 << 20) + 5, fill="pattern")
     try:
         for nwg, n in PUSH_CASES:
-            out, errs = P.run(mode, n, 5, nwg=nwg)
+            out, errs = P.run(mode, n, 5, nwg=nwg, stream=stream)
             assert not errs, (nwg, n, errs)
             for r in (0, 1):
                 pushes = mode != mpx.MODE_UNIDIR or r == 0
