@@ -64,10 +64,8 @@ struct XferArgs {
     int peer_slot;               // peer rank = its slot in my mailbox
     int nwg;                     // bulk push workgroups (same on both sides)
     int check;                   // 1 = checksum + poison each received payload
-    int ll_flags;                // bit0: 16-B stores (2 granules each), else 8-B;
-                                 // bit1: poll one sentinel granule first, then sweep
-                                 // bit2: re-read tx at every LL send (A/B of the
-                                 //       register-held payload)
+    int ll_flags;                // bit2: re-read tx at every LL send (A/B of the
+                                 //       register-held payload); other bits unused
     int ll_max;                  // messages <= ll_max bytes use LL (<= kLLMaxBytes);
                                  // same on both sides of the link
     int stream;                  // 1: bulk payload stores add the nt hint (sc0 sc1 nt)

@@ -188,6 +188,7 @@ __global__ void k_wait(const u64* flag, u64 v, Status* st, u64 timeout_ticks) {
 // k_xfer: the transfer loop.  One launch runs all `iters` iterations of one
 // rank's side; the peer runs its own launch on its own GPU at the same time.
 // ---------------------------------------------------------------------------
+template <int MODE>
 struct Loop {
     const XferArgs& a;
     int* s_abort;      // LDS: this workgroup gave up
@@ -232,7 +233,7 @@ struct Loop {
         return now_ticks() - t0 > a.timeout_ticks;
     }
 
-    __device__ bool is_ll(long long n) const { return a.mode != MPX_MODE_NONBLOCKING && n <= a.ll_max; }
+    __device__ bool is_ll(long long n) const { return MODE != MPX_MODE_NONBLOCKING && n <= a.ll_max; }
 
     // ---- send: push n bytes of tx[0:n) into the peer's rx -------------------
     // LL: one workgroup; every 16-B store carries two granules {payload:32,
@@ -242,17 +243,6 @@ struct Loop {
         const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;   // a 0-byte message is one empty granule
         const int nu = (ng + 1) >> 1;                      // 16-B units
         const unsigned tag = ll_tag(seq);
-        if (!(a.ll_flags & 1)) {   // one 8-B system-scope store per granule
-            u64* g = &a.peer_mb->ll[a.my_slot][0];
-            for (int k = threadIdx.x; k < ng; k += kBlock) {
-                const long long off = 4ll * k;
-                unsigned d = 0;
-                if (off + 4 <= n) d = *reinterpret_cast<const unsigned*>(a.tx + off);
-                else for (long long b = 0; off + b < n; ++b) d |= (unsigned)a.tx[off + b] << (8 * b);
-                st_sys(g + k, ((u64)tag << 32) | d);
-            }
-            return;
-        }
         const __amdgpu_buffer_rsrc_t dst = rsrc(&a.peer_mb->ll[a.my_slot][0], (unsigned)(nu * 16));
 #pragma unroll
         for (int j = 0; j < kLLUnitsPerLane; ++j) {
@@ -329,11 +319,11 @@ struct Loop {
     // LL receive: every lane issues the loads of ALL its units (up to 4)
     // back to back, then checks the tags — one memory round trip per poll,
     // not one per unit.
-    // 16-B form (ll_flags bit 0, default): one 16-B sc0|sc1 volatile load
-    // per unit, both granule tags checked (the sender tags both halves of
-    // every unit).  Against 8-B granule loads it halves the load count:
-    // 4 KiB ping-pong 4.32 -> 2.56 us per iteration (profiles/r01_ll_preload_ab.jsonl).
-    __device__ bool wait_ll16(long long n, u64 seq, int iter) const {
+    // One 16-B sc0|sc1 volatile load per unit, both granule tags checked
+    // (the sender tags both halves of every unit).  Against the earlier 8-B
+    // granule loads it halves the load count: 4 KiB ping-pong 4.32 -> 2.56 us
+    // per iteration (profiles/r01_ll_ab.jsonl, r01_ll_preload_ab.jsonl).
+    __device__ bool wait_ll(long long n, u64 seq, int iter) const {
         const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;
         const int nu = (ng + 1) >> 1;
         const int mine = nu > (int)threadIdx.x ? (nu - (int)threadIdx.x + kBlock - 1) / kBlock : 0;
@@ -365,62 +355,6 @@ struct Loop {
                     const u64 d = ((u64)x[j].z << 32) | x[j].x;
                     if (off + 8 <= n) {
                         *reinterpret_cast<u64*>(a.rx + off) = d;
-                    } else {
-                        for (long long b = 0; off + b < n; ++b) a.rx[off + b] = (unsigned char)(d >> (8 * b));
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        return !aborted();
-    }
-
-    __device__ bool wait_ll(long long n, u64 seq, int iter) const {
-        if ((a.ll_flags & 3) == 1) return wait_ll16(n, seq, iter);
-        constexpr int kPer = kLLGranules / kBlock;         // granules per lane, max
-        const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;
-        const int mine = ng > (int)threadIdx.x ? (ng - (int)threadIdx.x + kBlock - 1) / kBlock : 0;
-        const unsigned tag = ll_tag(seq);
-        const u64* g = &a.my_mb->ll[a.peer_slot][threadIdx.x];
-        u64 x[kPer];
-        if ((a.ll_flags & 2) && ng > 2) {
-            // sentinel: one lane polls the message's last granule before the
-            // whole workgroup sweeps (less polling traffic on the landing zone)
-            if (threadIdx.x == 0) {
-                const u64* last = &a.my_mb->ll[a.peer_slot][ng - 1];
-                const u64 t0 = now_ticks();
-                u64 spins = 0;
-                while ((unsigned)(ld_sys(last) >> 32) != tag) {
-                    if (should_stop(++spins, t0)) { give_up(iter); break; }
-                    __builtin_amdgcn_s_sleep(0);
-                }
-            }
-            __syncthreads();
-            if (aborted()) return false;
-        }
-        if (mine > 0) {
-            const u64 t0 = now_ticks();
-            u64 spins = 0;
-            for (;;) {
-#pragma unroll
-                for (int j = 0; j < kPer; ++j)
-                    if (j < mine) x[j] = ld_sys(g + j * kBlock);
-                bool ok = true;
-#pragma unroll
-                for (int j = 0; j < kPer; ++j)
-                    if (j < mine) ok &= (unsigned)(x[j] >> 32) == tag;
-                if (ok) break;
-                if (should_stop(++spins, t0)) { give_up(iter); break; }
-                __builtin_amdgcn_s_sleep(0);
-            }
-            if (blockIdx.x == 0 && !*s_abort) {
-#pragma unroll
-                for (int j = 0; j < kPer; ++j) {
-                    if (j >= mine) break;
-                    const long long off = 4ll * ((int)threadIdx.x + j * kBlock);
-                    const unsigned d = (unsigned)x[j];
-                    if (off + 4 <= n) {
-                        *reinterpret_cast<unsigned*>(a.rx + off) = d;
                     } else {
                         for (long long b = 0; off + b < n; ++b) a.rx[off + b] = (unsigned char)(d >> (8 * b));
                     }
@@ -533,25 +467,30 @@ struct Loop {
     }
 };
 
-__global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
+// One instantiation per (mode, side): each carries only its own loop, so
+// register pressure stays within 4 waves per SIMD (<= 128 VGPRs, no spills)
+// and four k_xfer workgroups fit on a CU — pairs that share one GPU
+// (loopback ranks, -g maps) keep every workgroup resident.
+template <int MODE, int GROUP>
+__global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     __shared__ int s_abort;
     __shared__ u64 lds4[4];
     extern __shared__ v4u s_tx[];            // a.stage: dynamic LDS = one chunk
     if (threadIdx.x == 0) s_abort = 0;
-    Loop L{a, &s_abort, lds4, s_tx, {}};
+    Loop<MODE> L{a, &s_abort, lds4, s_tx, {}};
     const long long n = a.len;
     if (a.stage) L.stage_tx(n);
     __syncthreads();
     // the size this side sends: B, or the 1-byte ack of unidir group 0
-    const long long send_len = (a.mode == MPX_MODE_UNIDIR && a.group == 0) ? 1 : n;
-    const bool ll_send = blockIdx.x == 0 && (a.ll_flags & 1) && L.is_ll(send_len);
+    const long long send_len = (MODE == MPX_MODE_UNIDIR && GROUP == 0) ? 1 : n;
+    const bool ll_send = blockIdx.x == 0 && L.is_ll(send_len);
     if (ll_send) L.preload_ll(send_len);
     const bool reload = ll_send && (a.ll_flags & 4);   // A/B knob (bit 2): re-read tx at every send
     u64 txs = a.tx_seq0, rxs = a.rx_seq0;
     int inflight = 0;
     for (int i = 0; i < a.iters; ++i) {
-        if (a.mode == MPX_MODE_PINGPONG) {            // mpi_perf.c:70-82
-            if (a.group == 1) {
+        if constexpr (MODE == MPX_MODE_PINGPONG) {    // mpi_perf.c:70-82
+            if constexpr (GROUP == 1) {
                 if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs);                      // Send(tx, B, tag 1)
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 2)
@@ -562,8 +501,8 @@ __global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
                 if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs);                      // Send(tx, B, tag 2)
             }
-        } else if (a.mode == MPX_MODE_UNIDIR) {        // mpi_perf.c:132-144
-            if (a.group == 1) {
+        } else if constexpr (MODE == MPX_MODE_UNIDIR) {  // mpi_perf.c:132-144
+            if constexpr (GROUP == 1) {
                 if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs);                      // Send(tx, B)
                 if (!L.recv(1, ++rxs, i)) break;       // Recv(rx, 1) — the ack
@@ -586,8 +525,8 @@ __global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
             }
         }
     }
-    if (a.mode == MPX_MODE_NONBLOCKING && inflight > 0 && !L.aborted())
-        L.wait_bulk(rxs + a.iters, a.iters - 1);       // final Waitall(inflight)
+    if constexpr (MODE == MPX_MODE_NONBLOCKING)
+        if (inflight > 0 && !L.aborted()) L.wait_bulk(rxs + a.iters, a.iters - 1);   // final Waitall(inflight)
 }
 
 // ---------------------------------------------------------------------------
@@ -595,7 +534,14 @@ __global__ __launch_bounds__(kBlock) void k_xfer(XferArgs a) {
 // ---------------------------------------------------------------------------
 hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
-    hipLaunchKernelGGL(k_xfer, dim3(grid), dim3(kBlock), (unsigned)a.stage, s, a);
+    void (*k)(XferArgs) = nullptr;
+    switch (a.mode) {
+        case MPX_MODE_PINGPONG: k = a.group ? k_xfer<MPX_MODE_PINGPONG, 1> : k_xfer<MPX_MODE_PINGPONG, 0>; break;
+        case MPX_MODE_UNIDIR: k = a.group ? k_xfer<MPX_MODE_UNIDIR, 1> : k_xfer<MPX_MODE_UNIDIR, 0>; break;
+        case MPX_MODE_NONBLOCKING: k = k_xfer<MPX_MODE_NONBLOCKING, 0>; break;   // both sides alike
+        default: return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), (unsigned)a.stage, s, a);
     return hipGetLastError();
 }
 

@@ -284,11 +284,14 @@ bool same_device(const Rank& a, const Rank& b) {
     return a.bus_id[0] && strcmp(a.bus_id, b.bus_id) == 0;
 }
 
-// LL protocol knobs (DESIGN.md "LL"): MPX_LL_FLAGS overrides for sweeps.
+// LL protocol A/B knob (DESIGN.md "LL"): MPX_LL_FLAGS=4 re-reads tx at every
+// LL send instead of holding the payload in registers.  The 8-B granule and
+// sentinel-poll variants of the first LL A/B (profiles/r01_ll_ab.jsonl) lost
+// and were removed.
 int ll_flags() {
     static const int f = [] {
         const char* v = getenv("MPX_LL_FLAGS");
-        return v ? atoi(v) : 1;   // default: 16-B stores, all lanes poll (LL A/B)
+        return v ? atoi(v) : 0;
     }();
     return f;
 }

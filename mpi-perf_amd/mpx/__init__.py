@@ -16,7 +16,8 @@ from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmpx.so")
+# MPX_LIB: load another build of the library (A/B of two builds in tools/)
+LIB_PATH = os.environ.get("MPX_LIB") or os.path.join(PKG_ROOT, "lib", "libmpx.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "mpx.h")
 
 # enum values (include/mpx.h)
