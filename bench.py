@@ -48,6 +48,7 @@ HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # roofline; the bidirectional figure is reported beside it.
 XGMI_LINK_PEAK_BIDIR_GBPS = 153.6
 XGMI_LINK_PEAK_GBPS = XGMI_LINK_PEAK_BIDIR_GBPS / 2
+EXTRAS_DEADLINE_S = 120      # comparison engines at N > 1 (see main)
 
 
 def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:
@@ -445,34 +446,55 @@ def main() -> None:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
         if "round0_sweep" in res:
             extras["round0_sweep"] = res["round0_sweep"]
-        if not args.no_extras:
-            for eng in ("sdma", "rccl"):
-                if eng == engine_used:
-                    continue
-                r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, max(10, iters // 5),
-                                 world - 1, 1, barrier_sync, latency=False)
-                extras[f"{eng}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
 
     value = total / elapsed / 1e9
+    line = {
+        "metric": "per-pair xGMI GB/s at 4 MB + 8 B latency us; all-pairs aggregate GB/s at 2/4/8 GPUs",
+        "value": round(value, 3),
+        "unit": metric_unit,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": config,
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "extras": extras,
+    }
+    if not one and not args.no_extras:
+        # The comparison engines (BASELINE config 4: kernel vs SDMA vs RCCL)
+        # run after the headline is measured, under a watchdog: should one of
+        # them hang (an RCCL bootstrap cannot be interrupted), every rank
+        # still ends and rank 0 still prints its line, without those numbers.
+        done, lock = threading.Event(), threading.Lock()
+
+        def on_deadline():
+            with lock:
+                if done.is_set():          # the extras finished in time
+                    return
+                if rank == 0:
+                    extras["comparison_engines"] = f"abandoned after {EXTRAS_DEADLINE_S} s"
+                    print(json.dumps(line), flush=True)
+                os._exit(0)
+
+        dog = threading.Timer(EXTRAS_DEADLINE_S, on_deadline)
+        dog.daemon = True
+        dog.start()
+        for eng in ("sdma", "rccl"):
+            if config["engine"].startswith(eng):
+                continue
+            r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, max(10, iters // 5),
+                             world - 1, 1, barrier_sync, latency=False)
+            extras[f"{eng}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
+        with lock:
+            done.set()
+        dog.cancel()
     if rank == 0:
-        line = {
-            "metric": "per-pair xGMI GB/s at 4 MB + 8 B latency us; all-pairs aggregate GB/s at 2/4/8 GPUs",
-            "value": round(value, 3),
-            "unit": metric_unit,
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": config,
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "extras": extras,
-        }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
