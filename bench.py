@@ -180,8 +180,11 @@ def tune_push_local(mpx, c, rounds, rank, tx, rx, nbytes, expect, expect_ack) ->
     rank's wall times (0.0 for a variant that does not apply)."""
     g, peer = round_role(rounds, 0, rank)
     times = []
+    # the one-GPU rehearsal stacks every rank on GPU 0: widths above 128
+    # would not leave every pair's workgroups resident together
+    max_wg = 128 if os.environ.get("MPX_BENCH_ONE_GPU") else 256
     for nwg, stream in PUSH_CANDIDATES:
-        if nbytes <= 8192 or nwg * 16 > nbytes:
+        if nbytes <= 8192 or nwg * 16 > nbytes or nwg > max_wg:
             times.append(0.0)
             continue
         c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 2, tx, rx, nbytes, check_payload=True, expect=expect[peer],

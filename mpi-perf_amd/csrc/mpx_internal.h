@@ -92,7 +92,10 @@ inline int bulk_nwg(long long len, bool same_device) {
     // cover the link's bandwidth-delay product), 16 KiB within one GPU.
     const long long per = same_device ? (16 << 10) : (32 << 10);
     long long n = (len + per - 1) / per;
-    const long long cap = same_device ? 256 : 128;
+    // within one GPU both kernels of a pair, and of every other pair that
+    // shares the GPU, must stay resident together: 128 keeps two pairs'
+    // check-mode launches (4 x 128 workgroups) at half the chip's 4 per CU
+    const long long cap = 128;
     if (n < 1) n = 1;
     if (n > cap) n = cap;
     return (int)n;
