@@ -491,8 +491,9 @@ def main() -> None:
         for eng in ("sdma", "rccl"):
             if config["engine"].startswith(eng):
                 continue
-            r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, max(10, iters // 5),
-                             world - 1, 1, barrier_sync, latency=False)
+            # 512 iterations: two graph-replayed SDMA chunks (run_sdma), no host-bound tail
+            r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
+                             latency=False)
             extras[f"{eng}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
         with lock:
             done.set()

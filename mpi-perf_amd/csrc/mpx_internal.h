@@ -106,7 +106,8 @@ hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s);
 hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int* grid_out);
 hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s);
 hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s);
-hipError_t launch_signal(u64* flag, u64 value, hipStream_t s);
-hipError_t launch_wait(const u64* flag, u64 value, Status* st, u64 timeout_ticks, hipStream_t s);
+hipError_t launch_signal(u64* flag, const u64* base, u64 value, hipStream_t s);
+hipError_t launch_wait(const u64* flag, const u64* base, u64 value, Status* st, u64 timeout_ticks, hipStream_t s);
+hipError_t launch_seqbase(u64* base, u64 tx, u64 rx, int add, hipStream_t s);
 
 }  // namespace mpx

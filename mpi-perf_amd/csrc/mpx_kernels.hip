@@ -165,23 +165,36 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const unsigned char* p, siz
 }
 
 // ---------------------------------------------------------------------------
-// SDMA-engine helpers: one lane stores / polls a mailbox flag.
+// SDMA-engine helpers: one lane stores / polls a mailbox flag.  The value is
+// v, plus *base when base is set: a graph-captured chunk of the loop
+// (run_sdma) carries sequence numbers relative to a device-side base that
+// k_seqbase sets before the first replay and advances at the end of each.
 // ---------------------------------------------------------------------------
-__global__ void k_signal(u64* flag, u64 v) {
-    if (threadIdx.x == 0) st_sys(flag, v);
+__device__ __forceinline__ u64 rel(const u64* base, u64 v) { return base ? ld_sys(base) + v : v; }
+
+__global__ void k_signal(u64* flag, const u64* base, u64 v) {
+    if (threadIdx.x == 0) st_sys(flag, rel(base, v));
 }
 
-__global__ void k_wait(const u64* flag, u64 v, Status* st, u64 timeout_ticks) {
+__global__ void k_wait(const u64* flag, const u64* base, u64 v, Status* st, u64 timeout_ticks) {
     if (threadIdx.x != 0) return;
+    const u64 want = rel(base, v);
     const u64 t0 = now_ticks();
     u64 spins = 0;
-    while (ld_sys(flag) < v) {
+    while (ld_sys(flag) < want) {
         if ((++spins & 255) == 0 && now_ticks() - t0 > timeout_ticks) {
             __hip_atomic_store(&st->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         __builtin_amdgcn_s_sleep(1);
     }
+}
+
+// base[0..1] = {tx, rx} (add = 0), or base[0..1] += {tx, rx} (add = 1)
+__global__ void k_seqbase(u64* base, u64 tx, u64 rx, int add) {
+    if (threadIdx.x != 0) return;
+    st_sys(base, add ? ld_sys(base) + tx : tx);
+    st_sys(base + 1, add ? ld_sys(base + 1) + rx : rx);
 }
 
 // ---------------------------------------------------------------------------
@@ -624,15 +637,21 @@ hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_signal(u64* flag, u64 value, hipStream_t s) {
+hipError_t launch_signal(u64* flag, const u64* base, u64 value, hipStream_t s) {
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
-    hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, s, flag, value);
+    hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, s, flag, base, value);
     return hipGetLastError();
 }
 
-hipError_t launch_wait(const u64* flag, u64 value, Status* st, u64 timeout_ticks, hipStream_t s) {
+hipError_t launch_wait(const u64* flag, const u64* base, u64 value, Status* st, u64 timeout_ticks, hipStream_t s) {
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
-    hipLaunchKernelGGL(k_wait, dim3(1), dim3(64), 0, s, flag, value, st, timeout_ticks);
+    hipLaunchKernelGGL(k_wait, dim3(1), dim3(64), 0, s, flag, base, value, st, timeout_ticks);
+    return hipGetLastError();
+}
+
+hipError_t launch_seqbase(u64* base, u64 tx, u64 rx, int add, hipStream_t s) {
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
+    hipLaunchKernelGGL(k_seqbase, dim3(1), dim3(64), 0, s, base, tx, rx, add);
     return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include <stdarg.h>
@@ -87,6 +88,10 @@ struct DeviceGuard {
 
 enum MailboxKind { kMbUncached = 0, kMbFine = 1, kMbCoarse = 2 };
 
+// (mode, group, peer rank, bytes, timeout ticks, iterations) of a captured
+// SDMA chunk
+typedef std::tuple<int, int, int, long long, u64, int> SdmaKey;
+
 struct Rank {
     bool local = false;
     bool imported = false;
@@ -109,6 +114,7 @@ struct Rank {
     u64 rx_seq[MPX_MAX_RANKS] = {};
     ncclComm_t comm = nullptr;
     int comm_rank = -1;
+    std::map<SdmaKey, hipGraphExec_t> sdma_graphs;   // run_sdma's captured chunks
 };
 
 struct RankDesc {
@@ -398,41 +404,6 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
 // engine: SDMA — hipMemcpyAsync into the peer's rx, then a one-lane flag
 // store; the receiver's stream waits on its mailbox flag with a one-lane poll.
 // ---------------------------------------------------------------------------
-struct SdmaOps {
-    Rank& me;
-    Rank& peer;
-    int my_slot, peer_slot;
-    u64 tmo;
-    int launches = 0;
-    // MPX_SDMA_SIGNAL=kernel|cp: flag store by a one-lane kernel (default) or
-    // by hipStreamWriteValue64.  Waits are always bounded one-lane kernels: a
-    // stream-level wait (hipStreamWaitValue64) cannot time out.
-    bool cp_signal = [] {
-        const char* v = getenv("MPX_SDMA_SIGNAL");
-        return v && !strcmp(v, "cp");
-    }();
-
-    int push(long long n, u64 seq) {
-        if (n > 0) {
-            HIPCK(hipMemcpyAsync(peer.rx, me.tx, (size_t)n, hipMemcpyDeviceToDevice, me.stream));
-            ++launches;
-        }
-        if (cp_signal) {
-            // command-processor write, ordered after the copy on this stream
-            HIPCK(hipStreamWriteValue64(me.stream, &peer.mb->flag[my_slot][0], seq, 0));
-        } else {
-            HIPCK(launch_signal(&peer.mb->flag[my_slot][0], seq, me.stream));
-        }
-        ++launches;
-        return MPX_OK;
-    }
-    int wait(u64 seq) {
-        HIPCK(launch_wait(&me.mb->flag[peer_slot][0], seq, me.status, tmo, me.stream));
-        ++launches;
-        return MPX_OK;
-    }
-};
-
 // check mode for the stream engines: checksum the received bytes into
 // csum[i], then poison them — stream-ordered before the next push.
 int stream_check(Rank& me, long long n, int i, int iters) {
@@ -443,6 +414,123 @@ int stream_check(Rank& me, long long n, int i, int iters) {
     return MPX_OK;
 }
 
+struct SdmaOps {
+    Rank& me;
+    Rank& peer;
+    int my_slot, peer_slot;
+    u64 tmo;
+    const u64* txb = nullptr;   // graph capture: seqs relative to these device words
+    const u64* rxb = nullptr;
+    int launches = 0;
+    // The flag store is a one-lane kernel ordered after the copy on this
+    // stream (hipStreamWriteValue64 measured slower, 10.9 vs 8.6 us per
+    // iteration, profiles/r01_sdma_signal_ab.jsonl).  Waits are bounded
+    // one-lane kernels: a stream-level wait (hipStreamWaitValue64) cannot
+    // time out.
+    int push(long long n, u64 seq) {
+        if (n > 0) {
+            HIPCK(hipMemcpyAsync(peer.rx, me.tx, (size_t)n, hipMemcpyDeviceToDevice, me.stream));
+            ++launches;
+        }
+        HIPCK(launch_signal(&peer.mb->flag[my_slot][0], txb, seq, me.stream));
+        ++launches;
+        return MPX_OK;
+    }
+    int wait(u64 seq) {
+        HIPCK(launch_wait(&me.mb->flag[peer_slot][0], rxb, seq, me.status, tmo, me.stream));
+        ++launches;
+        return MPX_OK;
+    }
+    // one iteration i of the loop (mpi_perf.c:70-82, 95-124, 132-144), seqs
+    // relative to tx0 / rx0; check mode checksums + poisons each received
+    // payload where the reference's Recv returns (before the reply / ack);
+    // *inflight is the non-blocking window fill
+    int step(int mode, int group, long long len, int i, int iters, u64 tx0, u64 rx0, bool check, int* inflight) {
+        if (mode == MPX_MODE_PINGPONG) {
+            if (group == 1) {
+                TRY(push(len, tx0 + i + 1));
+                TRY(wait(rx0 + i + 1));
+                if (check) TRY(stream_check(me, len, i, iters));
+            } else {
+                TRY(wait(rx0 + i + 1));
+                if (check) TRY(stream_check(me, len, i, iters));
+                TRY(push(len, tx0 + i + 1));
+            }
+        } else if (mode == MPX_MODE_UNIDIR) {
+            if (group == 1) {
+                TRY(push(len, tx0 + i + 1));
+                TRY(wait(rx0 + i + 1));
+                if (check) TRY(stream_check(me, 1, i, iters));
+            } else {
+                TRY(wait(rx0 + i + 1));
+                if (check) TRY(stream_check(me, len, i, iters));
+                TRY(push(1, tx0 + i + 1));                  // Send(tx, 1): always one byte
+            }
+        } else {
+            TRY(push(len, tx0 + i + 1));
+            if (*inflight == kNbWindow - 1) {
+                TRY(wait(rx0 + i));                          // Waitall(255): not slot 255's receive
+                *inflight = 0;
+            } else {
+                ++*inflight;
+            }
+        }
+        return MPX_OK;
+    }
+};
+
+// Graph-captured chunks of the SDMA loop (no check mode): the host enqueues
+// ~3 operations per iteration at ~3.5 us each, so the plain loop is
+// host-bound (9.4-10.4 us per ping-pong iteration on a loopback pair, 6.0 us
+// replayed, profiles/r01_sdma_graph_ab.jsonl); capture and instantiation
+// happen before the timed region.  Sequence numbers in a chunk are relative to
+// me.scratch[2..3], which k_seqbase sets before the first replay and each
+// chunk's last node advances by its iteration count.  Full chunks have
+// kSdmaChunk = 256 iterations, which keeps the non-blocking window (a flush
+// every 256 iterations) aligned with them; the remainder (< 256, no flush
+// inside) is one more captured chunk of its own length.
+constexpr int kSdmaChunk = kNbWindow;
+constexpr int kSdmaGraphMin = 16;   // fewer iterations: plain enqueue
+
+bool sdma_graphs_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("MPX_SDMA_GRAPH");
+        return !(v && atoi(v) == 0);
+    }();
+    return on;
+}
+
+int sdma_chunk_graph(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, long long len,
+                     u64 tmo, int count, hipGraphExec_t* out) {
+    const SdmaKey key{mode, group, peer_rank, len, tmo, count};
+    auto it = me.sdma_graphs.find(key);
+    if (it != me.sdma_graphs.end()) {
+        *out = it->second;
+        return MPX_OK;
+    }
+    SdmaOps cap{me, peer, my_rank, peer_rank, tmo, me.scratch + 2, me.scratch + 3};
+    HIPCK(hipStreamBeginCapture(me.stream, hipStreamCaptureModeThreadLocal));
+    int inflight = 0, st = MPX_OK;
+    for (int j = 0; j < count && st == MPX_OK; ++j) st = cap.step(mode, group, len, j, 0, 0, 0, false, &inflight);
+    if (st == MPX_OK) st = launch_seqbase(me.scratch + 2, count, count, 1, me.stream) == hipSuccess
+                               ? MPX_OK : fail(MPX_ERR_HIP, "k_seqbase launch in capture");
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(me.stream, &g);
+    if (st != MPX_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return st;
+    }
+    HIPCK(e);
+    hipGraphExec_t x = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIPCK(ei);
+    me.sdma_graphs[key] = x;
+    *out = x;
+    return MPX_OK;
+}
+
+
 int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters, long long len,
              const mpx_xfer_opts* o, mpx_timing* t) {
     SdmaOps op{me, peer, my_rank, peer_rank, timeout_ticks(o)};
@@ -450,50 +538,31 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     if (check) HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
     me.status->err = 0;
     me.status->where = 0;
-    u64 txs = me.tx_seq[peer_rank], rxs = me.rx_seq[peer_rank];
-    const u64 rxs0 = rxs;
+    const u64 txs0 = me.tx_seq[peer_rank], rxs0 = me.rx_seq[peer_rank];
+    // graph-replayed chunks for the bulk of the loop (not in check mode,
+    // whose per-iteration checksum slots would move with every chunk)
+    const bool graphs = !check && sdma_graphs_enabled() && iters >= kSdmaGraphMin;
+    const int chunks = graphs ? iters / kSdmaChunk : 0;
+    const int rest = graphs && iters % kSdmaChunk >= kSdmaGraphMin ? iters % kSdmaChunk : 0;
+    hipGraphExec_t full = nullptr, tail = nullptr;
+    if (chunks > 0) TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, kSdmaChunk, &full));
+    if (rest > 0) TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, rest, &tail));
+    if (full || tail) HIPCK(launch_seqbase(me.scratch + 2, txs0, rxs0, 0, me.stream));
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
+    for (int c = 0; c < chunks; ++c) HIPCK(hipGraphLaunch(full, me.stream));
+    if (tail) HIPCK(hipGraphLaunch(tail, me.stream));
     int inflight = 0;
-    for (int i = 0; i < iters; ++i) {
-        if (mode == MPX_MODE_PINGPONG) {
-            if (group == 1) {
-                TRY(op.push(len, ++txs));
-                TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, len, i, iters));
-            } else {
-                TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, len, i, iters));
-                TRY(op.push(len, ++txs));
-            }
-        } else if (mode == MPX_MODE_UNIDIR) {
-            if (group == 1) {
-                TRY(op.push(len, ++txs));
-                TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, 1, i, iters));
-            } else {
-                TRY(op.wait(++rxs));
-                if (check) TRY(stream_check(me, len, i, iters));
-                TRY(op.push(1, ++txs));                  // Send(tx, 1): always one byte
-            }
-        } else {
-            TRY(op.push(len, ++txs));
-            if (inflight == kNbWindow - 1) {
-                TRY(op.wait(rxs0 + i));
-                inflight = 0;
-            } else {
-                ++inflight;
-            }
-        }
-    }
-    if (mode == MPX_MODE_NONBLOCKING && inflight > 0) TRY(op.wait(rxs0 + iters));
+    const int replayed = chunks * kSdmaChunk + rest;
+    for (int i = replayed; i < iters; ++i) TRY(op.step(mode, group, len, i, iters, txs0, rxs0, check, &inflight));
+    if (mode == MPX_MODE_NONBLOCKING && iters > 0 && (iters % kNbWindow) != 0) TRY(op.wait(rxs0 + iters));
     HIPCK(hipEventRecord(me.ev1, me.stream));
     HIPCK(hipEventSynchronize(me.ev1));
     t->wall_s = now_s() - t0;
     float ms = 0;
     HIPCK(hipEventElapsedTime(&ms, me.ev0, me.ev1));
     t->device_s = ms * 1e-3;
-    t->launches = op.launches;
+    t->launches = op.launches + (chunks + (tail ? 1 : 0));   // graph replays count once each
     t->nwg = 0;
     t->protocol = kProtoSdma;
     if (__atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE)) {
@@ -629,6 +698,10 @@ int mpx_finalize(mpx_ctx* ctx) {
         }
     }
     DBG("finalize: streams drained\n");
+    for (int i = 0; i < MPX_MAX_RANKS; ++i) {
+        for (auto& kv : ctx->r[i].sdma_graphs) (void)hipGraphExecDestroy(kv.second);
+        ctx->r[i].sdma_graphs.clear();
+    }
     for (void* p : ctx->ipc_opened) {
         const hipError_t e = hipIpcCloseMemHandle(p);
         if (e != hipSuccess) DBG("finalize: hipIpcCloseMemHandle(%p): %s\n", p, hipGetErrorString(e));

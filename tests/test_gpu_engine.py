@@ -173,6 +173,29 @@ def test_push_widths_staged_and_unstaged(mode, stream):
         P.close()
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_sdma_graph_chunks_keep_sequence_state(mode):
+    """SDMA engine without check mode replays graph-captured 256-iteration
+    chunks (run_sdma) plus a plain remainder; the link's sequence numbers must
+    come out exactly where the plain loop leaves them, so a checked run after
+    it still validates every payload."""
+    P = Pairs("sdma", 1, 65541, fill="pattern")
+    try:
+        for n, iters in [(65541, 519), (8, 256), (4096, 300), (1, 3)]:
+            out, errs = P.run(mode, n, iters, check=False)
+            assert not errs, (n, iters, errs)
+            assert all(out[r].launches > 0 for r in (0, 1))
+            for r in (0, 1):
+                m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else n
+                assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (n, r)
+            out, errs = P.run(mode, n, 5, check=True)
+            assert not errs, (n, "checked run after chunks", errs)
+            if mode != mpx.MODE_NONBLOCKING:
+                assert all(out[r].check_failures == 0 and out[r].check_iters == 5 for r in (0, 1))
+    finally:
+        P.close()
+
+
 @pytest.mark.parametrize("name", ["pingpong_p2_b456131_i3", "unidir_p2_b4096_i7", "pingpong_p4_b8_i10",
                                   "unidir_p4_b456131_i3", "nonblocking_p2_b4096_i7", "defaults_unidir"])
 def test_receive_digest_matches_reference(name):

@@ -9,7 +9,7 @@ for rep in 1 2; do
   order="cur prev"; [ $rep = 2 ] && order="prev cur"
   for v in $order; do
     lib=mpi-perf_amd/lib/libmpx.so; [ $v = prev ] && lib=mpi-perf_amd/lib/libmpx_prev.so
-    MPX_LIB=$PWD/$lib ENGINES=kernel MODES=0,1,2 MAXLOG=22 timeout -k 10 200 python -u tools/xfer_sweep.py > gpurun_out/libab_tmp.jsonl 2>&1 || exit 1
+    MPX_LIB=$PWD/$lib ENGINES=${AB_ENGINES:-kernel} MODES=0,1,2 MAXLOG=${AB_MAXLOG:-22} timeout -k 10 200 python -u tools/xfer_sweep.py > gpurun_out/libab_tmp.jsonl 2>&1 || exit 1
     sed "s/^{/{\"lib\": \"$v\", \"rep\": $rep, /" gpurun_out/libab_tmp.jsonl >> gpurun_out/libab.jsonl
   done
 done
