@@ -189,3 +189,15 @@ def test_processes_mode_all_pairs_seeded_payloads(tmp_path):
     from mpx.schedule import all_pairs_rounds
     assert {(int(f[2]), int(f[6])) for f in side} == {p for rnd in all_pairs_rounds(4) for p in rnd}
     assert all(int(f[16]) == 0 and int(f[15]) == 5 for f in side)
+
+
+@pytest.mark.parametrize("mode_args", [[], ["-u", "1"], ["-x", "1"]])
+def test_sdma_engine_graph_chunks_from_concurrent_threads(tmp_path, mode_args):
+    """-e sdma without -c: every rank thread captures and replays its own
+    hipGraph chunks (run_sdma) while the other pair's threads do the same
+    (thread-local capture); records for every run, no timeouts."""
+    p, recs, side = run(tmp_path, ["-w", "4", "-e", "sdma", "-f", "@G1", "-n", "1", "-p", "2", "-r", "3", "-i", "300",
+                                   "-b", "4096", "-l", "@LOGS"] + mode_args, names="vm,vm,runsc,runsc", gpus="0,0,0,0")
+    assert p.returncode == 0, p.stderr[-600:]
+    assert len(recs) == 2 * 2               # runs 1..2, two senders each
+    assert all(int(f[8]) == 300 and int(f[7]) == 4096 for f in recs)
