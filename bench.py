@@ -371,7 +371,9 @@ def main() -> None:
 
     # MPX_BENCH_ONE_GPU=1: rehearse the N>1 path with every rank on GPU 0
     # (two processes on one card share it; the IPC + mailbox path is the same)
-    dev = 0 if os.environ.get("MPX_BENCH_ONE_GPU") else local
+    # A launcher that gives each process only its own GPU (HIP_VISIBLE_DEVICES
+    # per rank) leaves device 0 as that GPU.
+    dev = 0 if os.environ.get("MPX_BENCH_ONE_GPU") or torch.cuda.device_count() <= local else local
     torch.cuda.set_device(dev)
     dist = None
     if not one:
