@@ -69,6 +69,8 @@ struct XferArgs {
     int ll_max;                  // messages <= ll_max bytes use LL (<= kLLMaxBytes);
                                  // same on both sides of the link
     int stream;                  // 1: bulk payload stores add the nt hint (sc0 sc1 nt)
+    int nb_publish;              // non-blocking mode: drain + flag every nb_publish
+                                 // pushes (divides kNbWindow) and at the last
     int stage;                   // bytes of dynamic LDS holding this workgroup's
                                  // chunk of tx (0: bulk pushes read tx from HBM)
 };

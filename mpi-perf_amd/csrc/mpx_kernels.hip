@@ -301,7 +301,9 @@ struct Loop {
         for (; v < nv; v += kBlock) __builtin_amdgcn_raw_buffer_store_b128(src[v], dst, v * 16, 0, AUX);
     }
 
-    __device__ void push_bulk(long long n, u64 seq) const {
+    // publish = false: the stores are issued but not drained and no flag is
+    // stored (non-blocking mode publishes every a.nb_publish pushes, see k_xfer)
+    __device__ void push_bulk(long long n, u64 seq, bool publish = true) const {
         const int w = blockIdx.x;
         if (w >= a.nwg) return;
         long long lo, hi;
@@ -319,6 +321,7 @@ struct Loop {
                 __builtin_amdgcn_raw_buffer_store_b8(a.tx[lo + o], dst, o, 0, kAuxSys);
             }
         }
+        if (!publish) return;
         drain_stores();                 // every storing wave
         __syncthreads();
         if (threadIdx.x == 0) st_sys(&a.peer_mb->flag[a.my_slot][w], seq);
@@ -527,7 +530,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 L.send(1, ++txs);                      // Send(tx, 1)
             }
         } else {                                       // mpi_perf.c:95-124
-            L.send(n, ++txs);                          // Isend + Irecv, slot `inflight`
+            // Isend + Irecv, slot `inflight`.  A receiver waits only at the
+            // window flush (i = 255 mod 256) and at the end, so a push needs
+            // its drain + flag only every a.nb_publish iterations (a divisor
+            // of 256) and at the last one: the drain's link round trip is
+            // paid once per nb_publish pushes instead of once per push.
+            L.push_bulk(n, ++txs, (i + 1) % a.nb_publish == 0 || i + 1 == a.iters);
             if (inflight == kNbWindow - 1) {
                 // Waitall(255, ...): the receive posted in slot 255 (this
                 // iteration) is not among the 255 waited for (mpi_perf.c:110-111)

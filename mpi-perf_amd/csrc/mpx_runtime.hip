@@ -347,6 +347,13 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     }();
     a.stream = ((o && (o->flags & MPX_XFER_STREAM)) || env_stream) ? 1 : 0;
     a.ll_flags = ll_flags();
+    // MPX_NB_PUBLISH=k (a power of two <= 256; 1 = every push)
+    static const int nb_publish = [] {
+        const char* v = getenv("MPX_NB_PUBLISH");
+        const int k = v ? atoi(v) : 16;
+        return (k >= 1 && k <= kNbWindow && (kNbWindow % k) == 0) ? k : 16;
+    }();
+    a.nb_publish = nb_publish;
     a.ll_max = ll_max_bytes(same_device(me, peer));
     if (const char* v = getenv("MPX_LL_MAX")) a.ll_max = atoi(v) < kLLMaxBytes ? atoi(v) : kLLMaxBytes;
 
