@@ -302,6 +302,19 @@ int ll_flags() {
     return f;
 }
 
+// Non-blocking mode: a push is published (kernel engine: drained + flag;
+// SDMA engine: flag kernel) every nb_publish() pushes and at the last one —
+// receivers wait only at window flushes and at the end.
+// MPX_NB_PUBLISH=k (a divisor of 256; 1 = every push).
+int nb_publish() {
+    static const int k = [] {
+        const char* v = getenv("MPX_NB_PUBLISH");
+        const int x = v ? atoi(v) : 16;
+        return (x >= 1 && x <= kNbWindow && (kNbWindow % x) == 0) ? x : 16;
+    }();
+    return k;
+}
+
 u64 timeout_ticks(const mpx_xfer_opts* o) {
     const u64 ms = (o && o->timeout_ms) ? o->timeout_ms : 10000;
     return ms * 100000ull;   // s_memrealtime runs at 100 MHz
@@ -347,13 +360,7 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     }();
     a.stream = ((o && (o->flags & MPX_XFER_STREAM)) || env_stream) ? 1 : 0;
     a.ll_flags = ll_flags();
-    // MPX_NB_PUBLISH=k (a power of two <= 256; 1 = every push)
-    static const int nb_publish = [] {
-        const char* v = getenv("MPX_NB_PUBLISH");
-        const int k = v ? atoi(v) : 16;
-        return (k >= 1 && k <= kNbWindow && (kNbWindow % k) == 0) ? k : 16;
-    }();
-    a.nb_publish = nb_publish;
+    a.nb_publish = nb_publish();
     a.ll_max = ll_max_bytes(same_device(me, peer));
     if (const char* v = getenv("MPX_LL_MAX")) a.ll_max = atoi(v) < kLLMaxBytes ? atoi(v) : kLLMaxBytes;
 
@@ -434,11 +441,12 @@ struct SdmaOps {
     // iteration, profiles/r01_sdma_signal_ab.jsonl).  Waits are bounded
     // one-lane kernels: a stream-level wait (hipStreamWaitValue64) cannot
     // time out.
-    int push(long long n, u64 seq) {
+    int push(long long n, u64 seq, bool publish = true) {
         if (n > 0) {
             HIPCK(hipMemcpyAsync(peer.rx, me.tx, (size_t)n, hipMemcpyDeviceToDevice, me.stream));
             ++launches;
         }
+        if (!publish) return MPX_OK;
         HIPCK(launch_signal(&peer.mb->flag[my_slot][0], txb, seq, me.stream));
         ++launches;
         return MPX_OK;
@@ -474,7 +482,7 @@ struct SdmaOps {
                 TRY(push(1, tx0 + i + 1));                  // Send(tx, 1): always one byte
             }
         } else {
-            TRY(push(len, tx0 + i + 1));
+            TRY(push(len, tx0 + i + 1, (i + 1) % nb_publish() == 0 || i + 1 == iters));
             if (*inflight == kNbWindow - 1) {
                 TRY(wait(rx0 + i));                          // Waitall(255): not slot 255's receive
                 *inflight = 0;
@@ -518,7 +526,7 @@ int sdma_chunk_graph(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode,
     SdmaOps cap{me, peer, my_rank, peer_rank, tmo, me.scratch + 2, me.scratch + 3};
     HIPCK(hipStreamBeginCapture(me.stream, hipStreamCaptureModeThreadLocal));
     int inflight = 0, st = MPX_OK;
-    for (int j = 0; j < count && st == MPX_OK; ++j) st = cap.step(mode, group, len, j, 0, 0, 0, false, &inflight);
+    for (int j = 0; j < count && st == MPX_OK; ++j) st = cap.step(mode, group, len, j, count, 0, 0, false, &inflight);
     if (st == MPX_OK) st = launch_seqbase(me.scratch + 2, count, count, 1, me.stream) == hipSuccess
                                ? MPX_OK : fail(MPX_ERR_HIP, "k_seqbase launch in capture");
     hipGraph_t g = nullptr;
