@@ -21,8 +21,8 @@ import torch.distributed as dist  # noqa: E402
 
 import bench  # noqa: E402
 
-rank, world, port, scenario, outdir = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4],
-                                       sys.argv[5])
+# set by the __main__ block below, or by a worker that imports this module
+rank, scenario = 0, "ok"
 
 
 class Timing:
@@ -79,6 +79,8 @@ class FakeMpx:
 
         def rccl_init_rank(self, r, n, uid):
             assert uid == b"uid-from-rank-0"
+            if scenario == "rccl_hangs" and rank == 1:
+                time.sleep(600)            # an RCCL bootstrap that never returns
             if scenario == "all_fail" and rank == 1:
                 raise FakeError("ncclCommInitRank failed")
             FakeMpx.log.append(["rccl_init", r, n])
@@ -102,18 +104,21 @@ class FakeMpx:
             FakeMpx.log.append(["close", self.engine])
 
 
-dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-extras = {}
-out = {"rank": rank}
-try:
-    nbytes = 65536 if scenario == "tune" else 4096
-    res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, nbytes, 7, 5, 2,
-                                          dist.barrier, extras)
-    out.update(res=res, engine_used=used, extras=extras)
-except SystemExit as e:
-    out.update(exit=str(e))
-out["log"] = FakeMpx.log
-with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
-    json.dump(out, f)
-dist.barrier()
-dist.destroy_process_group()
+if __name__ == "__main__":
+    rank, world, port, scenario, outdir = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4],
+                                           sys.argv[5])
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    extras = {}
+    out = {"rank": rank}
+    try:
+        nbytes = 65536 if scenario == "tune" else 4096
+        res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, nbytes, 7, 5, 2,
+                                              dist.barrier, extras)
+        out.update(res=res, engine_used=used, extras=extras)
+    except SystemExit as e:
+        out.update(exit=str(e))
+    out["log"] = FakeMpx.log
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,0 +1,58 @@
+"""bench.py main() at N = 2 on CPU over gloo (tests/bench_main_worker.py):
+rank 0 prints exactly one JSON line carrying the contract's keys; when a
+comparison engine hangs (an RCCL bootstrap that never returns) the watchdog
+still ends every rank with status 0 and rank 0 still prints its line."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "extras"}
+
+
+def run(scenario, world=2):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ps = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        ps.append(subprocess.Popen([sys.executable, os.path.join(HERE, "bench_main_worker.py"), scenario, "--gpus",
+                                    str(world), "--steps", "3", "--warmup", "1"], stdout=subprocess.PIPE,
+                                   stderr=subprocess.PIPE, text=True, env=env))
+    outs = [p.communicate(timeout=120) for p in ps]
+    return [p.returncode for p in ps], outs
+
+
+def lines(stdout):
+    return [json.loads(x) for x in stdout.splitlines() if x.startswith("{")]
+
+
+def test_one_json_line_with_the_contract_keys():
+    rcs, outs = run("ok")
+    assert rcs == [0, 0], [o[1][-600:] for o in outs]
+    got = lines(outs[0][0])
+    assert len(got) == 1 and not lines(outs[1][0])
+    d = got[0]
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["scaling"] == "weak" and d["unit"] == "GB/s"
+    assert d["config"]["workload"] == "all_pairs_rounds_unidir" and d["config"]["engine"] == "kernel"
+    assert d["roofline"]["bound"] == "xgmi" and d["roofline"]["peak"] == 76.8
+    assert isinstance(d["extras"]["sdma_aggregate_GBps"], float)
+    assert isinstance(d["extras"]["rccl_aggregate_GBps"], float)
+
+
+def test_hung_comparison_engine_cannot_cost_the_line():
+    rcs, outs = run("rccl_hangs")
+    assert rcs == [0, 0], [o[1][-600:] for o in outs]
+    got = lines(outs[0][0])
+    assert len(got) == 1
+    d = got[0]
+    assert d["extras"]["comparison_engines"] == "abandoned after 5 s"
+    assert isinstance(d["extras"]["sdma_aggregate_GBps"], float)      # finished before RCCL hung
+    assert "rccl_aggregate_GBps" not in d["extras"]
