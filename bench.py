@@ -15,7 +15,11 @@ A "step" is one run of the reference's loop (mpi_perf.c:474-569: barrier ->
   schedule; each of the N/2 pairs moves `iters` x 4 MiB G1 -> G0 over xGMI
   with the 1-byte ack (mpi_perf.c:127-145).  value = sum of bytes over all
   pairs / T, with T the max over ranks (weak scaling: every GPU is in one
-  pair per step).
+  pair per step).  Before the timed steps every round is validated once
+  (check mode, seeded payloads) and the bulk push variant (workgroups per
+  push x streaming store hint) is tuned on round 0's links; after them come
+  the 8 B latency (10^5 ping-pong iterations), config 3's pair sweep, and the
+  SDMA and RCCL comparison engines under a watchdog.
 
 Rank 0 prints one JSON line.  `roofline` is computed for the dominant kernel
 from HIP-event time measured inside this process (libmpx records the events
