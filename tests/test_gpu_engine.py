@@ -324,3 +324,21 @@ def test_ll_full_landing_zone(monkeypatch, mode):
 
 
 PROTO_LL = 0
+
+
+@pytest.mark.parametrize("knobs", [
+    {"MPX_STAGE": "0", "MPX_NB_PUBLISH": "1", "MPX_SDMA_GRAPH": "0"},
+    {"MPX_PUSH_STREAM": "1", "MPX_LL_FLAGS": "4", "MPX_NB_PUBLISH": "256", "MPX_PUSH_WG": "7"},
+    {"MPX_LL_MAX": "8192", "MPX_NB_PUBLISH": "2"},
+])
+def test_env_knob_variants(knobs):
+    """The documented MPX_* knobs switch code paths that the
+    defaults never take: each set runs every mode on both engines, every
+    payload checked, in a process of its own (libmpx reads them once)."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, **knobs)
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "knob_worker.py")], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-1500:]
