@@ -110,6 +110,27 @@ def traffic_from_profile(workload: str) -> dict | None:
         return json.load(f)
 
 
+def runtime_copy_rate(torch, nbytes: int, iters: int) -> float:
+    """The HIP runtime's own device-to-device copy (torch's copy_ ->
+    hipMemcpyAsync) of the same B, for comparison with k_copy: HBM traffic
+    (2B per copy) / average time per copy, HIP events on torch's stream."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    a.fill_(7)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    per = e0.elapsed_time(e1) * 1e-3 / iters
+    del a, b
+    torch.cuda.empty_cache()
+    return round(2 * nbytes / per / 1e9, 1)
+
+
 def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: int = 3) -> dict:
     """Two ranks on GPU 0 (one host thread each): per-pair time of the loop."""
     with mpx.Context(2, engine) as c:
@@ -431,6 +452,7 @@ def main() -> None:
             extras["loopback_pingpong_8B_half_rtt_us"] = round(lat["per_iter_us"] / 2, 3)
             uni = loopback_pair(mpx, "kernel", mpx.MODE_UNIDIR, 4 << 20, 200)
             extras["loopback_unidir_4MiB_GBps"] = round((4 << 20) / (uni["per_iter_us"] * 1e-6) / 1e9, 2)
+            extras["runtime_copy_hbm_GBps"] = runtime_copy_rate(torch, nbytes, iters)
         c.close()
     else:
         workload = "all_pairs_rounds_unidir"
