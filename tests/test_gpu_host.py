@@ -201,3 +201,19 @@ def test_sdma_engine_graph_chunks_from_concurrent_threads(tmp_path, mode_args):
     assert p.returncode == 0, p.stderr[-600:]
     assert len(recs) == 2 * 2               # runs 1..2, two senders each
     assert all(int(f[8]) == 300 and int(f[7]) == 4096 for f in recs)
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+def test_processes_mode_eight_ranks_all_28_pairs(tmp_path, engine):
+    """BASELINE config 4's process structure on one GPU: eight mpx_perf
+    processes (one per rank, as under mpiexec -n 8), -a 1 circle-method
+    rounds (7 rounds x 4 pairs = all 28 pairs), seeded payloads, every
+    payload checked."""
+    names = ",".join(["vm"] * 4 + ["runsc"] * 4)
+    rcs, err, recs, side = run_procs(tmp_path, ["-e", engine, "-a", "1", "-f", "@G1", "-n", "1", "-p", "4", "-u", "1",
+                                                "-r", "8", "-i", "5", "-b", "65541", "-c", "2", "-l", "@LOGS"], 8, names)
+    assert rcs == [0] * 8, err[-800:]
+    assert len(re.findall(r"ROUND (\d+): ", err)) == 7
+    from mpx.schedule import all_pairs_rounds
+    assert {(int(f[2]), int(f[6])) for f in side} == {p for rnd in all_pairs_rounds(8) for p in rnd}
+    assert all(int(f[16]) == 0 and int(f[15]) == 5 for f in side)
