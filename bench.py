@@ -477,6 +477,9 @@ def main() -> None:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
         if "round0_sweep" in res:
             extras["round0_sweep"] = res["round0_sweep"]
+            bidir = res["round0_sweep"].get(f"nonblocking_{nbytes}")
+            if bidir:   # -x 1 at B: both directions of the pair's link (2B per iteration)
+                extras["per_pair_bidir_GBps"] = bidir["GBps"]
 
     value = total / elapsed / 1e9
     line = {
