@@ -473,6 +473,13 @@ def main() -> None:
         if res.get("push_tune"):
             extras["push_tune_GBps_per_pair"] = res["push_tune"]
         extras["per_pair_unidir_GBps"] = round(achieved, 2)
+        peer0 = round_role(all_pairs_rounds(world), 0, 0)[1]
+        if rank == 0 and not os.environ.get("MPX_BENCH_ONE_GPU") and torch.cuda.device_count() > max(dev, peer0):
+            # the path round 0's first pair takes (one process per GPU: local rank = GPU)
+            try:
+                extras["link_round0_pair0"] = dict(mpx.link_info(dev, peer0), gpus=[dev, peer0])
+            except Exception as e:  # noqa: BLE001
+                extras["link_round0_pair0"] = f"{type(e).__name__}: {e}"[:200]
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
         if "round0_sweep" in res:

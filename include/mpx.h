@@ -133,6 +133,13 @@ const char *mpx_last_error(void);
 /* number of visible GPUs (replaces MPI_Comm_size's role of sizing the job,
    mpi_perf.c:375, for the one-process/many-GPU launch) */
 int mpx_device_count(int *count);
+/* interconnect between two visible GPUs (no reference call does this; the
+   nearest is the peer-host lookup of mpi_perf.c:171-198, which names the
+   path a pair's bytes take): link_type is the HSA link type
+   (MPX_LINK_XGMI, MPX_LINK_PCIE, ...), hops the hop count */
+#define MPX_LINK_PCIE 2
+#define MPX_LINK_XGMI 4
+int mpx_link_info(int dev_a, int dev_b, int *link_type, int *hops);
 
 /* MPI_Init analogue (mpi_perf.c:372): a context able to address `nranks`
    ranks (<= MPX_MAX_RANKS) with the given engine. */

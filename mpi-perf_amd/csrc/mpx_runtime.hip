@@ -679,6 +679,18 @@ int mpx_device_count(int* count) {
     return MPX_OK;
 }
 
+int mpx_link_info(int dev_a, int dev_b, int* link_type, int* hops) {
+    if (!link_type || !hops) return fail(MPX_ERR_INVALID, "NULL argument");
+    TRY(check_dev(dev_a));
+    TRY(check_dev(dev_b));
+    if (dev_a == dev_b) return fail(MPX_ERR_INVALID, "device %d is both ends of the link", dev_a);
+    uint32_t t = 0, h = 0;
+    HIPCK(hipExtGetLinkTypeAndHopCount(dev_a, dev_b, &t, &h));
+    *link_type = (int)t;
+    *hops = (int)h;
+    return MPX_OK;
+}
+
 int mpx_init(int nranks, int engine, mpx_ctx** out) {
     if (!out) return fail(MPX_ERR_INVALID, "ctx out-pointer is NULL");
     *out = nullptr;

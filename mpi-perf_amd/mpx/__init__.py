@@ -74,6 +74,7 @@ _SIGS = {
     "mpx_strerror": (C.c_char_p, [C.c_int]),
     "mpx_last_error": (C.c_char_p, []),
     "mpx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "mpx_link_info": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mpx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "mpx_finalize": (C.c_int, [C.c_void_p]),
     "mpx_alloc": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]),
@@ -129,6 +130,16 @@ def device_count() -> int:
     n = C.c_int(0)
     check(lib().mpx_device_count(C.byref(n)), "mpx_device_count")
     return n.value
+
+
+LINK_TYPES = {0: "hypertransport", 1: "qpi", 2: "pcie", 3: "infiniband", 4: "xgmi"}
+
+
+def link_info(dev_a: int, dev_b: int) -> dict:
+    """mpx_link_info: the interconnect between two visible GPUs."""
+    t, h = C.c_int(0), C.c_int(0)
+    check(lib().mpx_link_info(dev_a, dev_b, C.byref(t), C.byref(h)), "mpx_link_info")
+    return {"type": LINK_TYPES.get(t.value, t.value), "hops": h.value}
 
 
 @dataclass

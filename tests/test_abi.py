@@ -43,6 +43,7 @@ def test_argument_validation_without_gpu():
     assert L.mpx_finalize(None) == mpx.ERR_INVALID
     assert L.mpx_xfer(None, 0, 1, 0, 1, 1, None, None, 8, None) == mpx.ERR_INVALID
     assert L.mpx_rccl_get_unique_id(None) == mpx.ERR_INVALID
+    assert L.mpx_link_info(0, 1, None, None) == mpx.ERR_INVALID
     assert b"NULL" in L.mpx_last_error() or L.mpx_last_error()
 
 
@@ -51,3 +52,4 @@ def test_header_constants_match_binding():
     assert "#define MPX_MAX_RANKS 16" in txt and mpx.MAX_RANKS == 16
     assert "#define MPX_RANK_DESC_BYTES 512" in txt
     assert "0x6d70695f70657266ULL" in txt and mpx.PATTERN_SEED == 0x6D70695F70657266
+    assert "#define MPX_LINK_XGMI 4" in txt and mpx.LINK_TYPES[4] == "xgmi"

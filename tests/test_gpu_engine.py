@@ -342,3 +342,17 @@ def test_env_knob_variants(knobs):
     p = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "knob_worker.py")], env=env,
                        capture_output=True, text=True, timeout=110)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-1500:]
+
+
+def test_link_info_between_visible_gpus():
+    """mpx_link_info: every pair of visible GPUs reports its interconnect
+    (xGMI, one hop, on an MI355X node); one GPU is not a link."""
+    n = mpx.device_count()
+    with pytest.raises(mpx.MpxError) as e:
+        mpx.link_info(0, 0)
+    assert e.value.status == mpx.ERR_INVALID
+    with pytest.raises(mpx.MpxError):
+        mpx.link_info(0, n)                       # not a visible device
+    for b in range(1, n):
+        li = mpx.link_info(0, b)
+        assert li["type"] in mpx.LINK_TYPES.values() and li["hops"] >= 1
