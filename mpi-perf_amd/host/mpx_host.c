@@ -345,3 +345,96 @@ int mpxh_ipv4(const char *host, char *out, size_t cap)
     snprintf(out, cap, "%s", ip);
     return 0;
 }
+
+/* ---- the Windows / MS-MPI variant (/root/reference/windows/mpi-perf.cpp) --
+   Same record, log name and run loop as mpi_perf.c; a different front end:
+   seven positional arguments, unidirectional only, groups keyed by IPv4
+   address with a whole-string match, the peer is the last match. */
+
+/* generate_uuid, windows/mpi-perf.cpp:175-184: the GUID is formatted with
+   snprintf(guid_str, sizeof(guid_str), ...) where guid_str is a char *, so
+   only sizeof(char *) - 1 = 7 characters survive: the first 7 hex digits of
+   Data1.  Job ids and log names of the Windows variant carry exactly that. */
+void mpxh_uuid_windows(char out[64])
+{
+    char full[37];
+    mpxh_uuid(full);
+    memset(out, 0, 64);
+    memcpy(out, full, sizeof(char *) - 1); /* what snprintf(out, sizeof(char *), ...) keeps */
+}
+
+/* parse_args, windows/mpi-perf.cpp:187-197, over main's defaults (:226-230):
+   argv[1..7] = group-1 address file, group size, ppn, iters, buffer size,
+   runs, log folder.  A missing argument makes the reference pass argv[argc]
+   (NULL) to strncpy / atoi: MPXH_PARSE_CRASH.  Arguments after the seven are
+   ignored by the reference; here they may carry the MI355X extension flags
+   (-w -g -e -a -c -S -t), never the reference's own letters. */
+int mpxh_parse_args_windows(mpxh_options *o, int argc, char **argv)
+{
+    if (argc < 8) return MPXH_PARSE_CRASH;
+    o->use_dotnet = 0; /* :226 */
+    o->uni_dir = 1;    /* :228 */
+    o->nonblocking = 0;
+    strncpy(o->group1_hostfile, argv[1], MPXH_MAX_HOST - 1);
+    o->group_size = atoi(argv[2]);
+    o->ppn = atoi(argv[3]);
+    o->iters = atoi(argv[4]);
+    o->buff_sz = atoi(argv[5]);
+    o->num_runs = atoi(argv[6]);
+    strncpy(o->logfolder, argv[7], MPXH_MAX_HOST - 1);
+    if (argc > 8) {
+        for (int i = 8; i < argc; ++i)
+            if (argv[i][0] == '-' && argv[i][1] && !argv[i][2] && strchr("fndpibuhrlx", argv[i][1]))
+                return MPXH_PARSE_USAGE;
+        mpxh_options x;
+        mpxh_defaults(&x);
+        const int st = mpxh_parse_args(&x, argc - 7, argv + 7);
+        if (st != MPXH_PARSE_OK) return st;
+        o->world = x.world;
+        o->engine = x.engine;
+        o->all_pairs = x.all_pairs;
+        o->check = x.check;
+        o->sweep_min = x.sweep_min;
+        o->sweep_max = x.sweep_max;
+        o->timeout_ms = x.timeout_ms;
+        memcpy(o->gpus, x.gpus, sizeof o->gpus);
+    }
+    mpxh_uuid_windows(o->uuid); /* :196 */
+    return MPXH_PARSE_OK;
+}
+
+/* windows/mpi-perf.cpp:249-261: fgets every line, newline cut off (:259) */
+char *mpxh_read_group1_windows(const char *path, int group_size)
+{
+    char *lines = mpxh_read_group1(path, group_size);
+    if (!lines) return NULL;
+    for (int i = 0; i < (group_size > 0 ? group_size : 0); ++i) {
+        char *ln = lines + (size_t)i * MPXH_MAX_HOST;
+        ln[strcspn(ln, "\n")] = '\0';
+    }
+    return lines;
+}
+
+/* windows/mpi-perf.cpp:283-289: my_strnicmp(my_ipaddr, line, MAX_HOST_SZ),
+   i.e. the whole address, case-insensitively (no prefix match) */
+int mpxh_in_group1_windows(const char *addr, const char *lines, int group_size)
+{
+    int g = 0;
+    for (int i = 0; i < group_size; i++)
+        if (mpxh_strnicmp(addr, lines + (size_t)i * MPXH_MAX_HOST, MPXH_MAX_HOST) == 0) g = 1;
+    return g;
+}
+
+/* MPI_Comm_split (windows/mpi-perf.cpp:292-295) and get_peer_info
+   (:114-133): the loop has no break, so the LAST other-group rank with the
+   same group rank wins.  With two groups and ranks numbered by world rank
+   there is at most one, so the pairs equal mpxh_pairing's. */
+void mpxh_pairing_windows(int world, const int *group, int *group_rank, int *group_size, int *peer)
+{
+    mpxh_pairing(world, group, group_rank, group_size, peer);
+    for (int r = 0; r < world; ++r) {
+        peer[r] = -1;
+        for (int i = 0; i < world; ++i)
+            if (group[i] != group[r] && group_rank[i] == group_rank[r]) peer[r] = i;
+    }
+}

@@ -47,7 +47,9 @@ typedef struct mpxh_options {
 enum {
     MPXH_PARSE_OK = 0,
     MPXH_PARSE_USAGE = 1,           /* unknown flag / -h: usage + abort      */
-    MPXH_PARSE_BAD_VALUE = 2        /* a value of a new flag is malformed    */
+    MPXH_PARSE_BAD_VALUE = 2,       /* a value of a new flag is malformed    */
+    MPXH_PARSE_CRASH = 3            /* the reference dereferences a missing
+                                       argument (Windows variant)           */
 };
 
 /* defaults of main(), mpi_perf.c:388-392 (+ the new fields) */
@@ -116,5 +118,17 @@ void mpxh_uuid(char out[37]);
 /* IPv4 of a host name: last AF_INET result like get_ipaddress,
    mpi_perf.c:171-198.  Returns 0 ok, -1 lookup failed. */
 int mpxh_ipv4(const char *host, char *out, size_t cap);
+
+/* ---- the Windows / MS-MPI variant, windows/mpi-perf.cpp ----------------- */
+/* 7-character job id (generate_uuid's sizeof(char *) truncation, :175-184) */
+void mpxh_uuid_windows(char out[64]);
+/* positional parse_args, :187-197, over main's defaults :226-230 */
+int mpxh_parse_args_windows(mpxh_options *o, int argc, char **argv);
+/* group-1 address lines with the newline cut off, :249-261 */
+char *mpxh_read_group1_windows(const char *path, int group_size);
+/* whole-address case-insensitive membership, :283-289 */
+int mpxh_in_group1_windows(const char *addr, const char *lines, int group_size);
+/* Comm_split + last-match peer, :114-133, :292-295 */
+void mpxh_pairing_windows(int world, const int *group, int *group_rank, int *group_size, int *peer);
 
 #endif

@@ -23,6 +23,18 @@
  * ranks span several hosts, the host name, like MPI_Get_processor_name; else
  * (one host) virtual host k = "<host>-<k>" for ranks [k*P, (k+1)*P).  With
  * -a 1 every run is one round of the circle-method all-pairs schedule.
+ *
+ * Built with -DMPX_WINDOWS_CLI (bin/mpx_perf_win), the front end is the
+ * Windows / MS-MPI variant's (/root/reference/windows/mpi-perf.cpp):
+ *
+ *   mpx_perf_win <group1-addresses> <group-size> <ppn> <iters> <buffer-size>
+ *                <runs> <logfolder> [-w N -g ... -e ... -a ... -c ... -t ...]
+ *
+ * unidirectional only, ranks grouped by IPv4 address (whole-string match),
+ * 7-character job id, INFO lines on stdout, no ingest hook and no
+ * REPORT_BANDWIDTH.  A rank's address is its processor name when that is a
+ * numeric IPv4 address, the host's address when the name is the host's own,
+ * and otherwise (a virtual host of one node) the name itself.
  */
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
@@ -37,6 +49,8 @@
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
+
+#include <arpa/inet.h>
 
 #include "../../include/mpx.h"
 #include "mpx_boot.h"
@@ -84,6 +98,13 @@ static int me;               /* this process's world rank (processes mode) */
 static int local_rank;       /* its node-local rank */
 static int multi_host;       /* the ranks span more than one host */
 static mpxb *boot;
+
+#ifdef MPX_WINDOWS_CLI
+static const int win_cli = 1; /* windows/mpi-perf.cpp front end */
+#else
+static const int win_cli = 0;
+#endif
+static char addr_of[MPXH_MAX_RANKS][MPXH_MAX_HOST]; /* Windows variant's group key */
 
 static double wtime(void) /* MPI_Wtime */
 {
@@ -141,6 +162,7 @@ static int node_local(int r)
 static void ingest_hook(int rank)
 {
     const char *cmd = getenv("MPX_INGEST_CMD");
+    if (win_cli) return; /* the Windows variant has no ingest hook */
     if (node_local(rank) != 0 || !cmd || !*cmd) return;
     if (system(cmd) == -1) fprintf(stderr, "ingest hook failed: %s\n", strerror(errno));
 }
@@ -369,7 +391,8 @@ int main(int argc, char **argv)
     me = procs ? lrank : 0;
 
     mpxh_defaults(&opt);
-    const int pst = mpxh_parse_args(&opt, argc, argv);
+    const int pst = win_cli ? mpxh_parse_args_windows(&opt, argc, argv) : mpxh_parse_args(&opt, argc, argv);
+    if (pst == MPXH_PARSE_CRASH) raise(SIGSEGV); /* strncpy(..., argv[argc] == NULL), windows/mpi-perf.cpp:189 */
     if (pst == MPXH_PARSE_USAGE) {
         if (is_root()) mpxh_print_usage(stderr);
         mpx_abort();
@@ -381,12 +404,13 @@ int main(int argc, char **argv)
         }
         mpx_abort();
     }
-    if (is_root()) fprintf(stderr, "UUID: %s\n", opt.uuid); /* mpi_perf.c:338 */
+    if (is_root() && !win_cli) fprintf(stderr, "UUID: %s\n", opt.uuid); /* mpi_perf.c:338 */
 #ifdef REPORT_BANDWIDTH
     report_bandwidth = 1;
 #else
     report_bandwidth = getenv("MPX_REPORT_BANDWIDTH") != NULL;
 #endif
+    if (win_cli) report_bandwidth = 0;
     if (getenv("MPX_LOG_REFRESH_SEC")) log_refresh_sec = atof(getenv("MPX_LOG_REFRESH_SEC"));
 
     if (procs) {
@@ -413,7 +437,8 @@ int main(int argc, char **argv)
     if (v) mpx_abort();
     char *group1 = NULL;
     if (is_root()) {
-        group1 = mpxh_read_group1(opt.group1_hostfile, opt.group_size);
+        group1 = win_cli ? mpxh_read_group1_windows(opt.group1_hostfile, opt.group_size)
+                         : mpxh_read_group1(opt.group1_hostfile, opt.group_size);
         if (!group1) {
             fprintf(stderr, "cannot open group1 file: %s\n", opt.group1_hostfile);
             if (!procs) mpx_abort();
@@ -466,10 +491,41 @@ int main(int argc, char **argv)
             snprintf(name_of[r], MPXH_MAX_HOST, "%s", host_of[r]); /* MPI_Get_processor_name */
         else
             mpxh_processor_name(name_of[r], host_of[r], r, opt.ppn, NULL);
-        group_of[r] = mpxh_in_group1(name_of[r], group1, opt.group_size);
+        if (win_cli) { /* get_ipaddress(myhostname), windows/mpi-perf.cpp:278-289 */
+            unsigned char a4[4];
+            if (inet_pton(AF_INET, name_of[r], a4) == 1)
+                snprintf(addr_of[r], MPXH_MAX_HOST, "%s", name_of[r]);
+            else if (!strcmp(name_of[r], host_of[r]))
+                snprintf(addr_of[r], MPXH_MAX_HOST, "%.*s", (int)strcspn(procs ? ip_of[r] : node_ip, ":"),
+                         procs ? ip_of[r] : node_ip);
+            else
+                snprintf(addr_of[r], MPXH_MAX_HOST, "%s", name_of[r]);
+            group_of[r] = mpxh_in_group1_windows(addr_of[r], group1, opt.group_size);
+        } else {
+            group_of[r] = mpxh_in_group1(name_of[r], group1, opt.group_size);
+        }
     }
-    mpxh_pairing(world, group_of, grank_of, gsize_of, peer_of);
+    if (win_cli)
+        mpxh_pairing_windows(world, group_of, grank_of, gsize_of, peer_of);
+    else
+        mpxh_pairing(world, group_of, grank_of, gsize_of, peer_of);
     free(group1);
+
+    if (win_cli && !opt.all_pairs) {
+        /* every rank prints its INFO line to stdout right after the pairing
+           (windows/mpi-perf.cpp:303-306); a rank without a peer dereferences
+           the NULL peer_node_info there */
+        for (int r = 0; r < world; ++r) {
+            if (procs && r != me) continue;
+            const int p = peer_of[r];
+            if (p < 0) raise(SIGSEGV);
+            char line[1024];
+            mpxh_format_info(line, sizeof line, name_of[r], r, world, group_of[r], gsize_of[r], grank_of[r], p,
+                             addr_of[r], name_of[p], addr_of[p]);
+            fputs(line, stdout);
+        }
+        fflush(stdout);
+    }
 
     if (!opt.all_pairs) {
         for (int r = 0; r < world; ++r) {
@@ -501,7 +557,7 @@ int main(int argc, char **argv)
             snprintf(ip_of[r], sizeof ip_of[r], "%s:gpu%d", node_ip, dev_of[r]);
         }
     }
-    if (!opt.all_pairs) {
+    if (!opt.all_pairs && !win_cli) {
         for (int r = 0; r < world; ++r) {
             if (procs && r != me) continue; /* every rank prints its own line, mpi_perf.c:460-461 */
             char line[1024];
@@ -510,7 +566,7 @@ int main(int argc, char **argv)
                              ip_of[r], name_of[p], ip_of[p]);
             fputs(line, stderr);
         }
-    } else if (is_root()) {
+    } else if (opt.all_pairs && is_root()) {
         for (int rd = 0; rd < world - 1; ++rd) {
             int pairs[MPXH_MAX_RANKS / 2][2];
             const int np = mpxh_round_pairs(world, rd, pairs);

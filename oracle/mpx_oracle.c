@@ -99,6 +99,36 @@ void oracle_pairing(int world, const int *group, int *group_rank, int *peer)
     }
 }
 
+/* windows/mpi-perf.cpp:28-46 (my_strnicmp, same as mpi_perf.c's), :256-260
+   (newline cut), :283-289 (n = MAX_HOST_SZ: the whole string) */
+int oracle_win_in_group1(const char *addr, const char *lines, int group_size)
+{
+    int g = 0;
+    char line[ORACLE_MAX_HOST];
+    for (int i = 0; i < group_size; i++) {
+        memcpy(line, lines + (size_t)i * ORACLE_MAX_HOST, ORACLE_MAX_HOST);
+        line[ORACLE_MAX_HOST - 1] = '\0';
+        line[strcspn(line, "\n")] = '\0';
+        if (oracle_strnicmp(addr, line, ORACLE_MAX_HOST) == 0) g = 1;
+    }
+    return g;
+}
+
+/* windows/mpi-perf.cpp:292-295 and :125-132 (no break: the last match) */
+void oracle_win_pairing(int world, const int *group, int *group_rank, int *peer)
+{
+    for (int r = 0; r < world; ++r) {
+        int gr = 0;
+        for (int q = 0; q < r; ++q) gr += group[q] == group[r];
+        group_rank[r] = gr;
+    }
+    for (int r = 0; r < world; ++r) {
+        peer[r] = -1;
+        for (int i = 0; i < world; ++i)
+            if (group[i] != group[r] && group_rank[i] == group_rank[r]) peer[r] = i;
+    }
+}
+
 /* mpi_perf.c:95-124 */
 long long oracle_nb_waited(long long iters)
 {

@@ -33,6 +33,17 @@ int oracle_in_group1(const char *name, int name_len, const char *lines, int grou
    the same group_rank, :225-233; -1 if none). */
 void oracle_pairing(int world, const int *group, int *group_rank, int *peer);
 
+/* --- the Windows / MS-MPI variant's group rule (windows/mpi-perf.cpp) ---
+   Restated from the source: that file needs MS-MPI and Winsock, so it cannot
+   be compiled here and this part of the oracle is parity-unpinned. */
+/* 1 if `addr` equals (case-insensitively, whole string) any of the
+   `group_size` MAX_HOST-strided lines after each line's newline is cut off
+   (:256-260, :283-289) */
+int oracle_win_in_group1(const char *addr, const char *lines, int group_size);
+/* Comm_split keyed by world rank (:292-295) and get_peer_info's loop without
+   a break: the LAST other-group rank with the same group rank (:114-133) */
+void oracle_win_pairing(int world, const int *group, int *group_rank, int *peer);
+
 /* --- transfer loops (mpi_perf.c:66-145), CPU engine -------------------- */
 enum { ORACLE_PINGPONG = 0, ORACLE_NONBLOCKING = 1, ORACLE_UNIDIR = 2 };
 typedef struct oracle_rank_stats {

@@ -217,3 +217,35 @@ def test_processes_mode_eight_ranks_all_28_pairs(tmp_path, engine):
     from mpx.schedule import all_pairs_rounds
     assert {(int(f[2]), int(f[6])) for f in side} == {p for rnd in all_pairs_rounds(8) for p in rnd}
     assert all(int(f[16]) == 0 and int(f[15]) == 5 for f in side)
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+def test_windows_front_end_runs_and_records(tmp_path, engine):
+    """bin/mpx_perf_win (windows/mpi-perf.cpp's positional command line):
+    unidirectional runs, records of runs 1.. by the group-1 rank, 7-character
+    job id in the records and the log name (:175-184, :333, :354-357), INFO
+    lines on stdout, every payload checked."""
+    win = os.path.join(ROOT, "mpi-perf_amd", "bin", "mpx_perf_win")
+    g1 = tmp_path / "group1"
+    g1.write_text("10.0.0.2\n")
+    logs = tmp_path / "logs"
+    env = dict(os.environ, MPX_PROCESSOR_NAMES="10.0.0.1,10.0.0.2")
+    p = subprocess.run([win, str(g1), "1", "1", "20", "65541", "4", str(logs), "-g", "0,0", "-e", engine,
+                        "-c", "1", "-t", "5000"], capture_output=True, text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr[-600:]
+    assert len(re.findall(r"^INFO: ", p.stdout, re.M)) == 2 and "UUID:" not in p.stderr
+    assert re.search(r"\[Run#: 0\]: Total time: ", p.stderr)
+    files = glob.glob(str(logs / "tcp-*.log"))
+    assert len(files) == 1
+    m = re.fullmatch(r"tcp-([0-9a-f]{7})-1-\d{4}-\d\d-\d\d-\d\d-\d\d-\d\d\.log", os.path.basename(files[0]))
+    assert m, files[0]
+    recs = [line.rstrip("\n").split(",") for line in open(files[0])]
+    assert [int(f[10]) for f in recs] == [1, 2, 3]
+    for f in recs:
+        assert f[1] == m[1] and f[2] == "1" and f[3] == "2" and f[6] == "1" and f[7] == "65541" and f[8] == "20"
+    side = []
+    for f in glob.glob(str(logs / "gpu-*.csv")):
+        side += [line.rstrip("\n").split(",") for line in open(f)][1:]
+    assert len(side) == 3
+    for f in side:
+        assert f[4] == "2" and int(f[15]) == 20 and int(f[16]) == 0   # unidir, 20 checked, 0 failures
