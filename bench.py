@@ -364,7 +364,23 @@ def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iter
     return res, engine_used
 
 
+def quiet_stdout() -> int:
+    """Route fd 1 to stderr for the rest of the run and return a duplicate
+    of the real stdout: libraries print banners there (RCCL's version block
+    at communicator init, HIP / RCCL debug output), and the driver reads
+    stdout for the ONE JSON line, which emit() writes to the duplicate."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    return real
+
+
+def emit(fd: int, line: dict) -> None:
+    os.write(fd, (json.dumps(line) + "\n").encode())
+
+
 def main() -> None:
+    out_fd = quiet_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -520,7 +536,7 @@ def main() -> None:
                     return
                 if rank == 0:
                     extras["comparison_engines"] = f"abandoned after {EXTRAS_DEADLINE_S} s"
-                    print(json.dumps(line), flush=True)
+                    emit(out_fd, line)
                 os._exit(0)
 
         dog = threading.Timer(EXTRAS_DEADLINE_S, on_deadline)
@@ -537,7 +553,7 @@ def main() -> None:
             done.set()
         dog.cancel()
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(out_fd, line)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

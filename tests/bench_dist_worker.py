@@ -83,6 +83,8 @@ class FakeMpx:
                 time.sleep(600)            # an RCCL bootstrap that never returns
             if scenario == "all_fail" and rank == 1:
                 raise FakeError("ncclCommInitRank failed")
+            # RCCL prints its version block on stdout at communicator init
+            os.write(1, b"RCCL version : 2.x (banner written by the library to fd 1)\n")
             FakeMpx.log.append(["rccl_init", r, n])
 
         def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,

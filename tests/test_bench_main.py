@@ -38,6 +38,10 @@ def test_one_json_line_with_the_contract_keys():
     assert rcs == [0, 0], [o[1][-600:] for o in outs]
     got = lines(outs[0][0])
     assert len(got) == 1 and not lines(outs[1][0])
+    # library output on fd 1 (the stand-in's RCCL banner) goes to stderr:
+    # stdout holds the JSON line and nothing else
+    assert outs[0][0].count("\n") == 1 and outs[1][0] == ""
+    assert "RCCL version" in outs[0][1]
     d = got[0]
     assert KEYS <= set(d)
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["scaling"] == "weak" and d["unit"] == "GB/s"
