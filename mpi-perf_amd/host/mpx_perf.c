@@ -354,6 +354,24 @@ static int needs_peer(int q)
     return opt.all_pairs || peer_of[me] == q;
 }
 
+/* The kernel and SDMA engines write into a peer's HBM: both ranks of every
+   pair this rank transfers with must be on its node.  Checked right after
+   the pairing, before any GPU call, like the reference's configuration
+   errors. */
+static void check_pairs_share_a_node(void)
+{
+    if (opt.engine == MPX_ENGINE_RCCL || opt.use_dotnet) return;
+    for (int q = 0; q < world; ++q) {
+        if (needs_peer(q) && strcmp(host_of[q], host_of[me]) != 0) {
+            fprintf(stderr,
+                    "rank %d (%s) and rank %d (%s) are on different hosts: the %s engine needs both on one node "
+                    "(use -e rccl)\n",
+                    me, host_of[me], q, host_of[q], mpxh_engine_name(opt.engine));
+            mpx_abort();
+        }
+    }
+}
+
 /* Map the peers' buffers (kernel / SDMA engines: IPC within one node) or
    join the RCCL communicator (rank 0's unique id, any number of nodes). */
 static void connect_ranks(void)
@@ -364,15 +382,6 @@ static void connect_ranks(void)
         if (mpxb_bcast0(boot, id, sizeof id) != 0) boot_failed();
         MPX_CHECK(mpx_rccl_init_rank(ctx, me, world, id));
         return;
-    }
-    for (int q = 0; q < world; ++q) {
-        if (needs_peer(q) && strcmp(host_of[q], host_of[me]) != 0) {
-            fprintf(stderr,
-                    "rank %d (%s) and rank %d (%s) are on different hosts: the %s engine needs both on one node "
-                    "(use -e rccl)\n",
-                    me, host_of[me], q, host_of[q], mpxh_engine_name(opt.engine));
-            mpx_abort();
-        }
     }
     static unsigned char all[MPXH_MAX_RANKS][MPX_RANK_DESC_BYTES];
     unsigned char mine[MPX_RANK_DESC_BYTES];
@@ -452,6 +461,9 @@ int main(int argc, char **argv)
     /* this process's host, IP and (processes mode) GPU */
     char node[MPXH_MAX_HOST] = {0};
     gethostname(node, sizeof node - 1);
+    /* MPX_HOSTNAME: the host name this process reports (multi-node rehearsal
+       on one machine: each process names a different "node") */
+    if (getenv("MPX_HOSTNAME") && *getenv("MPX_HOSTNAME")) snprintf(node, sizeof node, "%s", getenv("MPX_HOSTNAME"));
     char node_ip[MPXH_MAX_HOST] = "127.0.0.1";
     if (mpxh_ipv4(node, node_ip, sizeof node_ip) != 0) snprintf(node_ip, sizeof node_ip, "127.0.0.1");
     int ndev = world;
@@ -538,6 +550,7 @@ int main(int argc, char **argv)
         for (int r = 0; r < world; ++r)
             if (peer_of[r] < 0) mpx_abort();
     }
+    if (procs) check_pairs_share_a_node();
     if (!procs) { /* threads mode: rank r on GPU -g[r], else r mod #GPUs */
         if (!opt.use_dotnet) MPX_CHECK(mpx_device_count(&ndev));
         if (opt.gpus[0]) {

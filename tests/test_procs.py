@@ -161,3 +161,67 @@ def test_threads_mode_can_be_forced_under_a_launcher(tmp_path):
                        timeout=60)
     assert p.returncode == 0, p.stderr[-400:]
     assert len(INFO.findall(p.stderr)) == 2
+
+
+def run_nodes(tmp_path, args, hosts, lines=("nodeA",), extra_env=None):
+    """One mpx_perf process per rank; rank r reports host hosts[r]
+    (MPX_HOSTNAME) and its node-local rank, as a launcher spanning several
+    nodes would start them (multi-node rehearsal on one machine)."""
+    g1 = tmp_path / "group1"
+    g1.write_text("".join(x + "\n" for x in lines))
+    argv = [a.replace("@G1", str(g1)).replace("@LOGS", str(tmp_path / "logs")) for a in args]
+    port = free_port()
+    ps = []
+    n = len(hosts)
+    for r in range(n):
+        local = hosts[:r].count(hosts[r])
+        env = dict(os.environ, MPX_RANK=str(r), MPX_SIZE=str(n), MPX_LOCAL_RANK=str(local),
+                   MPX_BOOTSTRAP=f"127.0.0.1:{port}", MPX_PROCESSOR_NAMES="", MPX_HOSTNAME=hosts[r],
+                   MPX_BOOTSTRAP_TIMEOUT="30", HIP_VISIBLE_DEVICES="")
+        env.update(extra_env or {})
+        ps.append(subprocess.Popen([PERF] + argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                   env=env, cwd=tmp_path))
+    outs = [p.communicate(timeout=120) for p in ps]
+    return [p.returncode for p in ps], [o[1] for o in outs]
+
+
+def test_multi_node_groups_by_host_name(tmp_path):
+    """Ranks on two nodes: the processor name is the host
+    name, as MPI_Get_processor_name gives it (mpi_perf.c:433-434), so the -f
+    file lists nodes and --map-by ppr:2:node pairs rank k with rank 2+k, the
+    reference's pingpong_p2 layout.  The ingest hook runs on node-local rank 0
+    of the group-1 node only (mpi_perf.c:355-365, :378-384)."""
+    ref = CASES["pingpong_p2_b8_i10"]
+    rcs, errs = run_nodes(tmp_path, ["-f", "@G1", "-n", "1", "-p", "2", "-d", "1", "-r", "2", "-i", "10", "-b", "8",
+                                     "-l", "@LOGS"], ["nodeA", "nodeA", "nodeB", "nodeB"],
+                          extra_env={"MPX_INGEST_CMD": "touch ingest-$MPX_RANK"})
+    assert rcs == [0] * 4, errs
+    allerr = "".join(errs)
+    info = INFO.findall(allerr)
+    assert sorted((int(x[1]), int(x[3]), int(x[4]), int(x[5]), int(x[6])) for x in info) == \
+        sorted((d["rank"], d["group"], d["group_size"], d["group_rank"], d["peer"]) for d in ref["info"])
+    assert {(int(x[1]), x[0]) for x in info} == {(0, "nodeA"), (1, "nodeA"), (2, "nodeB"), (3, "nodeB")}
+    assert sorted(p.name for p in tmp_path.glob("ingest-*")) == ["ingest-0"]
+
+
+def test_kernel_engine_refuses_a_pair_across_nodes(tmp_path):
+    """The kernel and SDMA engines write into the peer's HBM: a pair spanning
+    two nodes is a configuration error, reported before any GPU call; the
+    RCCL engine passes the check (and here, without a GPU, stops at the
+    device query)."""
+    args = ["-f", "@G1", "-n", "1", "-p", "1", "-u", "1", "-r", "2", "-l", "@LOGS"]
+    for engine in ("kernel", "sdma"):
+        rcs, errs = run_nodes(tmp_path, args + ["-e", engine], ["nodeA", "nodeB"])
+        assert rcs == [255, 255], errs
+        assert "are on different hosts: the %s engine needs both on one node (use -e rccl)" % engine in "".join(errs)
+    rcs, errs = run_nodes(tmp_path, args + ["-e", "rccl"], ["nodeA", "nodeB"])
+    assert "different hosts" not in "".join(errs)
+    assert all(rc != 0 for rc in rcs) and "hipGetDeviceCount" in "".join(errs)
+
+
+def test_same_node_pairs_pass_the_node_check(tmp_path):
+    rcs, errs = run_nodes(tmp_path, ["-f", "@G1", "-n", "1", "-p", "1", "-u", "1", "-r", "2", "-l", "@LOGS"],
+                          ["nodeA", "nodeA"], lines=("nodeA-0",),
+                          extra_env={"MPX_PROCESSOR_NAMES": "nodeA-0,nodeA-1"})
+    assert "different hosts" not in "".join(errs)
+    assert "hipGetDeviceCount" in "".join(errs)
