@@ -356,3 +356,53 @@ def test_link_info_between_visible_gpus():
     for b in range(1, n):
         li = mpx.link_info(0, b)
         assert li["type"] in mpx.LINK_TYPES.values() and li["hops"] >= 1
+
+
+INT_MAX = (1 << 31) - 1    # the largest buff_len the reference's int accepts (mpi_perf.c:283, :464)
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+def test_max_size_pairs_every_mode(engine):
+    """B = 2^31 - 1 (golden `max_int_buffer`'s size) in every mode, seeded
+    payloads, every payload checked: chunk offsets and buffer-resource sizes
+    stay within 32 bits; nwg = 1 pushes one 2 GiB - 1 chunk."""
+    P = Pairs(engine, 1, INT_MAX, fill="seeded")
+    try:
+        for mode in MODES:
+            for nwg in ((0, 1) if engine == "kernel" else (0,)):
+                out, errs = P.run(mode, INT_MAX, 2, timeout_ms=30000, nwg=nwg)
+                assert not errs, (mode, nwg, errs)
+                for r in (0, 1):
+                    if mode != mpx.MODE_NONBLOCKING:
+                        assert out[r].check_iters == 2 and out[r].check_failures == 0, (mode, nwg, r)
+                    m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else INT_MAX
+                    assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (mode, nwg, r)
+    finally:
+        P.close()
+
+
+def test_copy_beyond_4gib(ctx):
+    """A copy past 2^32 bytes (64-bit unit indices, > 2^20 workgroups) against
+    the oracle's pattern checksum; nothing written past the end."""
+    n = (4 << 30) + 13
+    key = mpx.pattern_key(mpx.PATTERN_SEED, 9, 9, 9)
+    src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
+    try:
+        ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
+        ctx.fill(dst, n + 64, mpx.FILL_BYTE, 0xEE)
+        ctx.copy(0, dst, src, n, 1)
+        assert ctx.checksum(dst, n) == ctx.checksum(src, n)
+        assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
+        # the oracle's fill words over a window at the end (word k =
+        # mix64((key ^ k) + G), oracle_fill): word indices above 2^29
+        lo = n - 4096 - 13
+        got = ctx.read(dst, n - lo, offset=lo)
+        G = 0x9E3779B97F4A7C15
+        want = bytearray()
+        for k in range(lo // 8, (n + 7) // 8):
+            want += (O.lib().oracle_mix64(((key ^ k) + G) & 0xFFFFFFFFFFFFFFFF)).to_bytes(8, "little")
+        start = lo - (lo // 8) * 8
+        assert got == bytes(want[start:start + (n - lo)])
+    finally:
+        ctx.free(src)
+        ctx.free(dst)
