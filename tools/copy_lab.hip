@@ -144,10 +144,15 @@ template <int T, int U> void runD(const void* s, void* d, size_t n, int g, int, 
 int main(int argc, char** argv) {
     const size_t n = argc > 1 ? strtoull(argv[1], 0, 0) : (1ull << 30);
     const char* only = argc > 2 ? argv[2] : nullptr;
-    void *s, *d;
+    // optional placement offsets (argv[3] dst, argv[4] src, bytes): where the
+    // two buffers sit relative to each other in the HBM channel interleave
+    const size_t doff = argc > 3 ? strtoull(argv[3], 0, 0) : 0, soff = argc > 4 ? strtoull(argv[4], 0, 0) : 0;
+    void *s, *d, *s0, *d0;
     unsigned* bad;
-    CK(hipMalloc(&s, n));
-    CK(hipMalloc(&d, n));
+    CK(hipMalloc(&s0, n + soff));
+    CK(hipMalloc(&d0, n + doff));
+    s = (char*)s0 + soff;
+    d = (char*)d0 + doff;
     CK(hipMalloc(&bad, 4));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -198,8 +203,8 @@ int main(int argc, char** argv) {
             sum += gbps;
             if (gbps > best) best = gbps;
         }
-        printf("{\"variant\": \"%s\", \"bytes\": %zu, \"hbm_GBps_best\": %.1f, \"hbm_GBps_mean\": %.1f, \"bad_words\": %u}\n",
-               v.name, n, best, sum / 5, nb);
+        printf("{\"variant\": \"%s\", \"bytes\": %zu, \"dst_off\": %zu, \"src_off\": %zu, \"hbm_GBps_best\": %.1f, \"hbm_GBps_mean\": %.1f, \"bad_words\": %u}\n",
+               v.name, n, doff, soff, best, sum / 5, nb);
         fflush(stdout);
     }
     return 0;
