@@ -114,6 +114,29 @@ template <int T, int U> void runE(const void* s, void* d, size_t n, int, int, hi
     const size_t n16 = n / 16, g = (n16 + T * U - 1) / (T * U);
     hipLaunchKernelGGL((kE<T, U>), dim3((unsigned)g), dim3(T), 0, st, (const v4u*)s, (v4u*)d, n16);
 }
+// R / W: one-direction ceilings of the same shape (one 16-B unit per lane,
+// one step per workgroup): R reads src (nontemporal) and folds it into one
+// word per workgroup; W stores a constant.  Timed traffic is B per launch;
+// the lab's rate column counts 2B, so halve it for these two.
+__global__ __launch_bounds__(256) void kR(const v4u* __restrict__ s, v4u* __restrict__ d, size_t n16) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    v4u r = {0, 0, 0, 0};
+    if (i < n16) r = __builtin_nontemporal_load(s + i);
+    unsigned x = r.x ^ r.y ^ r.z ^ r.w;
+    for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o);
+    if (x == 0x9e3779b9u && threadIdx.x == 0) d[blockIdx.x] = r;   // keeps the loads live
+}
+__global__ __launch_bounds__(256) void kW(const v4u* __restrict__, v4u* __restrict__ d, size_t n16) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const v4u v = {(unsigned)i, 1u, 2u, 3u};
+    if (i < n16) __builtin_nontemporal_store(v, d + i);
+}
+void runR(const void* s, void* d, size_t n, int, int, hipStream_t st) {
+    hipLaunchKernelGGL(kR, dim3((unsigned)((n / 16 + 255) / 256)), dim3(256), 0, st, (const v4u*)s, (v4u*)d, n / 16);
+}
+void runW(const void* s, void* d, size_t n, int, int, hipStream_t st) {
+    hipLaunchKernelGGL(kW, dim3((unsigned)((n / 16 + 255) / 256)), dim3(256), 0, st, (const v4u*)s, (v4u*)d, n / 16);
+}
 // M: the runtime's own device-to-device copy
 void runM(const void* s, void* d, size_t n, int, int, hipStream_t st) { (void)hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, st); }
 
@@ -173,6 +196,8 @@ int main(int argc, char** argv) {
         {"A_t256_u1_nt_g262144", 262144, 256, runA<256, 1, true>},
         {"A_t512_u1_nt_g131072", 131072, 512, runA<512, 1, true>},
         {"M_hipMemcpyAsync_D2D", 0, 0, runM},
+        {"R_read_only (rate x0.5 = read GB/s)", 0, 256, runR},
+        {"W_write_only (rate x0.5 = write GB/s)", 0, 256, runW},
         {"A_t256_u2_nt_g65536 (product, again)", 65536, 256, runA<256, 2, true>},
         {"E_t256_u1 (again)", 0, 256, runE<256, 1>},
         {"E_t512_u1 (again)", 0, 512, runE<512, 1>},
