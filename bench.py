@@ -110,6 +110,24 @@ def traffic_from_profile(workload: str) -> dict | None:
         return json.load(f)
 
 
+def hbm_one_direction_ceiling() -> dict | None:
+    """Read-only and write-only HBM rates of k_copy's access shape (one 16-B
+    nontemporal unit per lane, one step per workgroup), measured by
+    tools/copy_lab into profiles/r01_copy_lab_read_write_ceilings.jsonl: what
+    HBM delivers in one direction on this part, beside the 8 TB/s spec."""
+    path = os.path.join(ROOT, "profiles", "r01_copy_lab_read_write_ceilings.jsonl")
+    if not os.path.exists(path):
+        return None
+    best = {}
+    with open(path) as f:
+        for line in f:
+            d = json.loads(line)
+            for key, tag in (("read", "R_read_only"), ("write", "W_write_only")):
+                if d["variant"].startswith(tag):   # the lab's column counts 2B per launch
+                    best[key] = max(best.get(key, 0.0), round(d["hbm_GBps_best"] / 2, 1))
+    return dict(best, source="profiles/r01_copy_lab_read_write_ceilings.jsonl") if best else None
+
+
 def runtime_copy_rate(torch, nbytes: int, iters: int) -> float:
     """The HIP runtime's own device-to-device copy (torch's copy_ ->
     hipMemcpyAsync) of the same B, for comparison with k_copy: HBM traffic
@@ -469,6 +487,9 @@ def main() -> None:
             uni = loopback_pair(mpx, "kernel", mpx.MODE_UNIDIR, 4 << 20, 200)
             extras["loopback_unidir_4MiB_GBps"] = round((4 << 20) / (uni["per_iter_us"] * 1e-6) / 1e9, 2)
             extras["runtime_copy_hbm_GBps"] = runtime_copy_rate(torch, nbytes, iters)
+        ceil = hbm_one_direction_ceiling()
+        if ceil:
+            extras["hbm_one_direction_ceiling_GBps"] = ceil
         c.close()
     else:
         workload = "all_pairs_rounds_unidir"
