@@ -249,6 +249,33 @@ def pick_push(torch, dist, times: list[float], nbytes: int) -> tuple[tuple[int, 
     return best, {push_name(*k): round(v, 2) for k, v in rates.items()}
 
 
+def pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, launch_bytes) -> dict:
+    """Every pair the timed steps covered (all N(N-1)/2 once the steps span
+    the N-1 rounds): its G1 launch rate, "g1>g0" -> GB/s averaged over the
+    steps that ran its round; and each round's aggregate, pairs x bytes /
+    the max over ranks of the loop's wall time, averaged over its steps.
+    Gathered after the timed region (one gloo all_gather)."""
+    mine = torch.tensor(step_dev + step_wall, dtype=torch.float64)
+    every = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    rates, agg = {}, {}
+    for s in range(steps):
+        rd = s % len(rounds)
+        walls = [float(every[r][steps + s]) for r in range(world)]
+        agg.setdefault(rd, []).append((world // 2) * launch_bytes / max(walls) / 1e9)
+        for r in range(world):
+            g, peer = round_role(rounds, rd, r)
+            if g == 1 and float(every[r][s]) > 0:
+                rates.setdefault(f"{r}>{peer}", []).append(launch_bytes / float(every[r][s]) / 1e9)
+    per_pair = {k: round(statistics.mean(v), 2) for k, v in sorted(rates.items(), key=lambda kv: tuple(
+        int(x) for x in kv[0].split(">")))}
+    out = {"pair_GBps": per_pair,
+           "round_aggregate_GBps": [round(statistics.mean(agg[rd]), 2) for rd in sorted(agg)]}
+    if per_pair:
+        out["pair_GBps_min_max"] = [min(per_pair.values()), max(per_pair.values())]
+    return out
+
+
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
                 latency=True, tune=True) -> dict:
     """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers).
@@ -326,13 +353,16 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     for s in range(warmup):
         step(s)
     dev_s, n_sends = 0.0, 0
+    step_dev, step_wall = [0.0] * steps, [0.0] * steps   # this rank's G1 device time / wall time per step
     barrier_sync()
     t0 = time.perf_counter()
     for s in range(steps):
         g, t = step(s)
+        step_wall[s] = t.wall_s
         if g == 1:
             dev_s += t.device_s
             n_sends += 1
+            step_dev[s] = t.device_s
     barrier_sync()
     elapsed = time.perf_counter() - t0
     tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -343,6 +373,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     dist.all_reduce(st, op=dist.ReduceOp.SUM)
     out["per_launch_s"] = float(st[0]) / max(float(st[1]), 1.0)
     out["per_pair_GBps"] = nbytes * iters / out["per_launch_s"] / 1e9
+    out.update(pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, nbytes * iters))
     if latency:
         g, peer = round_role(rounds, 0, rank)
         dist.barrier()
@@ -510,6 +541,10 @@ def main() -> None:
         if res.get("push_tune"):
             extras["push_tune_GBps_per_pair"] = res["push_tune"]
         extras["per_pair_unidir_GBps"] = round(achieved, 2)
+        extras["pairs_covered"] = len(res.get("pair_GBps", {}))
+        extras["pair_unidir_GBps"] = res.get("pair_GBps")
+        extras["pair_unidir_GBps_min_max"] = res.get("pair_GBps_min_max")
+        extras["round_aggregate_GBps"] = res.get("round_aggregate_GBps")
         peer0 = round_role(all_pairs_rounds(world), 0, 0)[1]
         if rank == 0 and not os.environ.get("MPX_BENCH_ONE_GPU") and torch.cuda.device_count() > max(dev, peer0):
             # the path round 0's first pair takes (one process per GPU: local rank = GPU)

@@ -60,3 +60,21 @@ def test_hung_comparison_engine_cannot_cost_the_line():
     assert d["extras"]["comparison_engines"] == "abandoned after 5 s"
     assert isinstance(d["extras"]["sdma_aggregate_GBps"], float)      # finished before RCCL hung
     assert "rccl_aggregate_GBps" not in d["extras"]
+
+
+def test_every_pair_of_four_ranks_has_a_rate():
+    """N = 4, 3 steps = the 3 rounds: all 6 pairs get a G1 launch rate
+    (bytes x iters / that rank's device time) and every round an aggregate."""
+    rcs, outs = run("ok", world=4)
+    assert rcs == [0] * 4, [o[1][-600:] for o in outs]
+    d = lines(outs[0][0])[0]
+    e = d["extras"]
+    assert e["pairs_covered"] == 6 and len(e["round_aggregate_GBps"]) == 3
+    pairs = {tuple(sorted(map(int, k.split(">")))) for k in e["pair_unidir_GBps"]}
+    assert pairs == {(a, b) for a in range(4) for b in range(a + 1, 4)}
+    launch = d["config"]["bytes"] * d["config"]["iters_per_step"]
+    for k, v in e["pair_unidir_GBps"].items():
+        g1 = int(k.split(">")[0])
+        assert abs(v - launch / (0.001 * (1 + g1)) / 1e9) < 0.01     # the stand-in's device time
+    assert e["pair_unidir_GBps_min_max"] == [min(e["pair_unidir_GBps"].values()),
+                                             max(e["pair_unidir_GBps"].values())]
