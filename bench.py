@@ -276,6 +276,31 @@ def pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, lau
     return out
 
 
+PAIR_LATENCY_ITERS = 10_000
+
+
+def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
+    """8 B ping-pong half round trip of every pair, round by round
+    (PAIR_LATENCY_ITERS iterations each): "g1>g0" -> us, the pair's slower
+    side's wall time / (2 x iterations)."""
+    walls = []
+    for rd in range(len(rounds)):
+        g, peer = round_role(rounds, rd, rank)
+        dist.barrier()
+        walls.append(c.xfer(mpx.MODE_PINGPONG, g, rank, peer, PAIR_LATENCY_ITERS, tx, rx, 8).wall_s)
+    mine = torch.tensor(walls, dtype=torch.float64)
+    every = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    out = {}
+    for rd in range(len(rounds)):
+        for r in range(world):
+            g, peer = round_role(rounds, rd, r)
+            if g == 1:
+                w = max(float(every[r][rd]), float(every[peer][rd]))
+                out[f"{r}>{peer}"] = round(w / (2 * PAIR_LATENCY_ITERS) * 1e6, 3)
+    return dict(sorted(out.items(), key=lambda kv: tuple(int(x) for x in kv[0].split(">"))))
+
+
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
                 latency=True, tune=True) -> dict:
     """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers).
@@ -381,6 +406,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         lat = torch.tensor([lt.wall_s], dtype=torch.float64)
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
         out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / (2 * LATENCY_ITERS) * 1e6, 3)
+        out["pair_pingpong_8B_half_rtt_us"] = pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx)
         out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes)
     dist.barrier()
     c.close()
@@ -554,6 +580,7 @@ def main() -> None:
                 extras["link_round0_pair0"] = f"{type(e).__name__}: {e}"[:200]
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
+            extras["pair_pingpong_8B_half_rtt_us"] = res["pair_pingpong_8B_half_rtt_us"]
         if "round0_sweep" in res:
             extras["round0_sweep"] = res["round0_sweep"]
             bidir = res["round0_sweep"].get(f"nonblocking_{nbytes}")

@@ -74,13 +74,16 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
     g1 = [round_role(rounds, s % (world - 1), r)[0] for r in range(world) for s in range(steps)]
     assert sum(g1) == (world // 2) * steps
     # the ping-pong latency probe ran on round 0 with 10^5 iterations of 8 B,
-    # then the round-0 size sweep (config 3: unidir and full-duplex -x 1)
+    # then every round's pairs with 10^4, then the round-0 size sweep (config 3: unidir and full-duplex -x 1)
     for d in res:
         r = d["rank"]
         pp = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0]
-        assert len(pp) == 1 and pp[0][6] == 100_000 and pp[0][7] == 8
+        assert len(pp) == world and pp[0][6] == 100_000 and pp[0][7] == 8
+        # then 10^4 iterations of 8 B on every round: every pair's latency
+        for rd, x in enumerate(pp[1:]):
+            assert (x[3], x[5], x[6], x[7]) == (*round_role(rounds, rd, r), 10_000, 8)
         g, peer = round_role(rounds, 0, r)
-        sweep = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel" and not x[8]][warmup + steps + 1:]
+        sweep = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel" and not x[8]][warmup + steps + world:]
         sizes = [1, 8, 64, 512, 4096]                        # config 3's sizes <= B (B = 4096 here)
         assert [x[7] for x in sweep] == [m for m in sizes for _ in (0, 1)]
         assert [x[2] for x in sweep] == [2, 1] * len(sizes)  # -u 1 then -x 1 at every size

@@ -78,3 +78,11 @@ def test_every_pair_of_four_ranks_has_a_rate():
         assert abs(v - launch / (0.001 * (1 + g1)) / 1e9) < 0.01     # the stand-in's device time
     assert e["pair_unidir_GBps_min_max"] == [min(e["pair_unidir_GBps"].values()),
                                              max(e["pair_unidir_GBps"].values())]
+
+
+def test_every_pair_has_a_latency():
+    rcs, outs = run("ok", world=4)
+    assert rcs == [0] * 4, [o[1][-600:] for o in outs]
+    lat = lines(outs[0][0])[0]["extras"]["pair_pingpong_8B_half_rtt_us"]
+    assert {tuple(sorted(map(int, k.split(">")))) for k in lat} == {(a, b) for a in range(4) for b in range(a + 1, 4)}
+    assert all(v == round(0.002 / (2 * 10_000) * 1e6, 3) for v in lat.values())    # the stand-in's wall time
