@@ -214,7 +214,19 @@ def push_name(nwg: int, stream: bool) -> str:
     return f"{nwg}{'+nt' if stream else ''}"
 
 
-def tune_push_local(mpx, c, rounds, rank, tx, rx, nbytes, expect, expect_ack) -> list[float]:
+def one_gpu_push_cap(world: int) -> int:
+    """MPX_BENCH_ONE_GPU stacks all `world` ranks on GPU 0, and the two
+    halves of every pair must have all their workgroups resident at once.
+    k_xfer fits 4 workgroups per CU (1024 on 256 CUs); capping each side's
+    push width at 512 / world keeps the N/2 concurrent pairs at <= 512 of
+    them (N = 8: 64 each), with room for other work on the card.  0 when
+    every rank has its own GPU."""
+    if not os.environ.get("MPX_BENCH_ONE_GPU"):
+        return 0
+    return max(16, min(128, 512 // max(world, 1)))
+
+
+def tune_push_local(mpx, c, rounds, rank, world, tx, rx, nbytes, expect, expect_ack) -> list[float]:
     """Time round 0's unidir loop at B once per bulk push variant (width =
     workgroups per push, mpx_xfer_opts.nwg; streaming store hint), each
     variant's payloads first validated (check mode, 2 iterations).  No
@@ -223,9 +235,7 @@ def tune_push_local(mpx, c, rounds, rank, tx, rx, nbytes, expect, expect_ack) ->
     rank's wall times (0.0 for a variant that does not apply)."""
     g, peer = round_role(rounds, 0, rank)
     times = []
-    # the one-GPU rehearsal stacks every rank on GPU 0: widths above 128
-    # would not leave every pair's workgroups resident together
-    max_wg = 128 if os.environ.get("MPX_BENCH_ONE_GPU") else 256
+    max_wg = one_gpu_push_cap(world) or 256
     for nwg, stream in PUSH_CANDIDATES:
         if nbytes <= 8192 or nwg * 16 > nbytes or nwg > max_wg:
             times.append(0.0)
@@ -348,7 +358,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
                 c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True,
                        expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000)
             if engine == "kernel" and tune:
-                tune_times = tune_push_local(mpx, c, rounds, rank, tx, rx, nbytes, [d[1] for d in descs],
+                tune_times = tune_push_local(mpx, c, rounds, rank, world, tx, rx, nbytes, [d[1] for d in descs],
                                              [d[2] for d in descs])
         except Exception as e:  # noqa: BLE001
             err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
@@ -477,6 +487,14 @@ def main() -> None:
     nbytes = args.bytes or ((1 << 30) if one else (4 << 20))
     iters = args.iters or (10 if one else 500)
 
+    if os.environ.get("MPX_BENCH_ONE_GPU") and world > 1:
+        # All ranks on one card: every process's HW queues share the card's
+        # queue slots.  At N = 8 the default (4 per process, plus each rank's
+        # CU-masked stream) oversubscribes them; a queue the scheduler has
+        # not mapped cannot run the half of a pair its peer is waiting on,
+        # and the peer's device deadline fires.  One queue per process (the
+        # CU-masked rank stream keeps its own) fits.  Set before HIP starts.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
     # CPU baseline first, before this process touches the GPU
     cpu = None
     if one and rank == 0 and not args.no_cpu_baseline:
@@ -490,6 +508,10 @@ def main() -> None:
     # A launcher that gives each process only its own GPU (HIP_VISIBLE_DEVICES
     # per rank) leaves device 0 as that GPU.
     dev = 0 if os.environ.get("MPX_BENCH_ONE_GPU") or torch.cuda.device_count() <= local else local
+    if one_gpu_push_cap(world) and "MPX_PUSH_WG" not in os.environ:
+        # the default push width too (validation, steps, sweep), before the
+        # library first reads it
+        os.environ["MPX_PUSH_WG"] = str(one_gpu_push_cap(world))
     torch.cuda.set_device(dev)
     dist = None
     if not one:
