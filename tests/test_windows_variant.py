@@ -191,3 +191,28 @@ def test_extension_flags_after_positionals(tmp_path):
     p = run(tmp_path, ["@G1", "1", "2", "10", "100", "2", "@LOGS", "-w", "4"],
             names="10.0.0.1,10.0.0.1,10.0.0.2,10.0.0.2")
     assert len(INFO.findall(p.stdout)) == 4
+
+
+def test_processes_mode_info_per_rank(tmp_path):
+    """Under a launcher (one process per rank, the reference's mpiexec model)
+    every process prints its own INFO line on stdout; rank 0's options and
+    group file reach the others (MPI_Bcast, windows/mpi-perf.cpp:264-274)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    g1 = tmp_path / "group1"
+    g1.write_text("10.0.0.2\n")
+    ps = []
+    for r in range(2):
+        env = dict(os.environ, MPX_RANK=str(r), MPX_SIZE="2", MPX_LOCAL_RANK=str(r), MPX_BOOTSTRAP=f"127.0.0.1:{port}",
+                   MPX_PROCESSOR_NAMES="10.0.0.1,10.0.0.2", MPX_BOOTSTRAP_TIMEOUT="30", HIP_VISIBLE_DEVICES="")
+        # only rank 0 reads the file: the other rank names one that does not exist
+        ps.append(subprocess.Popen([WIN, str(g1) if r == 0 else str(tmp_path / "absent"), "1", "1", "10", "100", "2",
+                                    str(tmp_path / "logs")], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                   text=True, env=env))
+    outs = [p.communicate(timeout=60) for p in ps]
+    infos = [INFO.findall(o[0]) for o in outs]
+    assert [len(i) for i in infos] == [1, 1], [o[1][-300:] for o in outs]
+    assert [(int(i[0][1]), int(i[0][3]), int(i[0][6])) for i in infos] == [(0, 0, 1), (1, 1, 0)]
