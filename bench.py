@@ -287,6 +287,32 @@ def pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, lau
 
 
 PAIR_LATENCY_ITERS = 10_000
+# BASELINE config 4's other workload, scripts/run-hbv3.sh: -u 1 -b 456131 -i 10
+HBV3_BYTES, HBV3_ITERS, HBV3_PASSES = 456131, 10, 3
+
+
+def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
+    """run-hbv3's message shape over the all-pairs rounds: every round runs
+    the unidir loop at 456131 B x 10 iterations behind a barrier, HBV3_PASSES
+    passes; a round's aggregate is pairs x B x iterations / the max over ranks
+    of the loop's wall time (the reference's MAX allreduce), median over the
+    passes.  At 10 iterations launch and flag latency weigh as much as the
+    link: this is the reference's own short-loop measurement."""
+    walls = []
+    for _ in range(HBV3_PASSES):
+        for rd in range(len(rounds)):
+            g, peer = round_role(rounds, rd, rank)
+            dist.barrier()
+            walls.append(c.xfer(mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES).wall_s)
+    w = torch.tensor(walls, dtype=torch.float64)
+    dist.all_reduce(w, op=dist.ReduceOp.MAX)
+    nr = len(rounds)
+    per_round = []
+    for rd in range(nr):
+        t = statistics.median(float(w[p * nr + rd]) for p in range(HBV3_PASSES))
+        per_round.append(round((world // 2) * HBV3_BYTES * HBV3_ITERS / t / 1e9, 2))
+    return dict(bytes=HBV3_BYTES, iters=HBV3_ITERS, round_aggregate_GBps=per_round,
+                mean_aggregate_GBps=round(statistics.mean(per_round), 2))
 
 
 def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
@@ -418,6 +444,8 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / (2 * LATENCY_ITERS) * 1e6, 3)
         out["pair_pingpong_8B_half_rtt_us"] = pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx)
         out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes)
+        if nbytes >= HBV3_BYTES:
+            out["hbv3_rounds"] = hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx)
     dist.barrier()
     c.close()
     dist.barrier()   # see above: all imports closed before the next allocation
@@ -603,6 +631,8 @@ def main() -> None:
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
             extras["pair_pingpong_8B_half_rtt_us"] = res["pair_pingpong_8B_half_rtt_us"]
+        if "hbv3_rounds" in res:
+            extras["hbv3_rounds_unidir"] = res["hbv3_rounds"]
         if "round0_sweep" in res:
             extras["round0_sweep"] = res["round0_sweep"]
             bidir = res["round0_sweep"].get(f"nonblocking_{nbytes}")

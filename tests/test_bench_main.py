@@ -86,3 +86,14 @@ def test_every_pair_has_a_latency():
     lat = lines(outs[0][0])[0]["extras"]["pair_pingpong_8B_half_rtt_us"]
     assert {tuple(sorted(map(int, k.split(">")))) for k in lat} == {(a, b) for a in range(4) for b in range(a + 1, 4)}
     assert all(v == round(0.002 / (2 * 10_000) * 1e6, 3) for v in lat.values())    # the stand-in's wall time
+
+
+def test_hbv3_shaped_rounds():
+    """run-hbv3's -u 1 -b 456131 -i 10 over every round (config 4's short
+    loop): one aggregate per round, median of the passes."""
+    rcs, outs = run("ok", world=4)
+    assert rcs == [0] * 4, [o[1][-600:] for o in outs]
+    h = lines(outs[0][0])[0]["extras"]["hbv3_rounds_unidir"]
+    assert h["bytes"] == 456131 and h["iters"] == 10 and len(h["round_aggregate_GBps"]) == 3
+    # the stand-in's wall time is 2 ms: 2 pairs x 456131 B x 10 / 2 ms
+    assert all(abs(v - 2 * 456131 * 10 / 0.002 / 1e9) < 0.05 for v in h["round_aggregate_GBps"])
