@@ -174,13 +174,39 @@ def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: in
         return dict(median_s=statistics.median(res[1:]), per_iter_us=statistics.median(res[1:]) / iters * 1e6)
 
 
+POST_TIMEOUT_MS = 2000
+
+
+def safe_wall(c, errs: list, *xfer_args) -> float:
+    """Wall time of one transfer measured after the headline (latency,
+    sweeps); a failure there (a device deadline, a refused transfer) is
+    recorded in `errs` and returns +inf, so this rank still takes part in
+    every collective that follows and the headline line is still printed."""
+    try:
+        # a 2 s per-wait deadline (the longest wait here is one 4 MiB push):
+        # a broken link costs each later partner 2 s, not the default 10
+        return c.xfer(*xfer_args, timeout_ms=POST_TIMEOUT_MS).wall_s
+    except Exception as e:  # noqa: BLE001
+        errs.append(f"{type(e).__name__}: {e}"[:240])
+        return float("inf")
+
+
+def finite(x: float, digits: int):
+    return round(x, digits) if x != float("inf") and x == x else None
+
+
+def rate(num: float, wall: float, digits: int):
+    """num / wall, or None when the wall time is a failed transfer's +inf"""
+    return finite(num / wall, digits) if wall != float("inf") else None
+
+
 # BASELINE config 3 / SURVEY §8d cfg3: the pair sweep uses config 1's sizes
 # (the reference's own CPU sweep) plus the reference's default B = 456131
 CFG3_SIZES = (1, 8, 64, 512, 4096, 32768, 262144, 456131, 1 << 20, 4 << 20)
 LATENCY_ITERS = 100_000     # cfg3: 8 B latency with I >= 10^5
 
 
-def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes) -> dict:
+def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs) -> dict:
     """Config 3 beside the headline: the pairs of round 0 at every cfg3 size
     <= B, unidirectional (`-u 1`, B per iteration) and bidirectional (`-x 1`
     full duplex, 2B per iteration, mpi_perf.c:538).  Time = max over ranks of
@@ -190,17 +216,16 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes) -> dict:
 
     def timed(mode, n, it):
         dist.barrier()
-        t = c.xfer(mode, g, rank, peer, it, tx, rx, n)
-        w = torch.tensor([t.wall_s], dtype=torch.float64)
+        w = torch.tensor([safe_wall(c, errs, mode, g, rank, peer, it, tx, rx, n)], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         return float(w[0])
 
     for n in sorted(set(x for x in CFG3_SIZES if x <= nbytes) | {nbytes}):
         it = max(20, min(2000, (256 << 20) // n))
         w = timed(mpx.MODE_UNIDIR, n, it)
-        rates[f"unidir_{n}"] = dict(us_per_iter=round(w / it * 1e6, 3), GBps=round(n * it / w / 1e9, 3))
+        rates[f"unidir_{n}"] = dict(us_per_iter=finite(w / it * 1e6, 3), GBps=rate(n * it / 1e9, w, 3))
         w = timed(mpx.MODE_NONBLOCKING, n, it)
-        rates[f"nonblocking_{n}"] = dict(us_per_iter=round(w / it * 1e6, 3), GBps=round(2 * n * it / w / 1e9, 3))
+        rates[f"nonblocking_{n}"] = dict(us_per_iter=finite(w / it * 1e6, 3), GBps=rate(2 * n * it / 1e9, w, 3))
     return rates
 
 
@@ -291,7 +316,7 @@ PAIR_LATENCY_ITERS = 10_000
 HBV3_BYTES, HBV3_ITERS, HBV3_PASSES = 456131, 10, 3
 
 
-def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
+def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
     """run-hbv3's message shape over the all-pairs rounds: every round runs
     the unidir loop at 456131 B x 10 iterations behind a barrier, HBV3_PASSES
     passes; a round's aggregate is pairs x B x iterations / the max over ranks
@@ -303,19 +328,20 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
         for rd in range(len(rounds)):
             g, peer = round_role(rounds, rd, rank)
             dist.barrier()
-            walls.append(c.xfer(mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES).wall_s)
+            walls.append(safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES))
     w = torch.tensor(walls, dtype=torch.float64)
     dist.all_reduce(w, op=dist.ReduceOp.MAX)
     nr = len(rounds)
     per_round = []
     for rd in range(nr):
         t = statistics.median(float(w[p * nr + rd]) for p in range(HBV3_PASSES))
-        per_round.append(round((world // 2) * HBV3_BYTES * HBV3_ITERS / t / 1e9, 2))
+        per_round.append(rate((world // 2) * HBV3_BYTES * HBV3_ITERS / 1e9, t, 2))
+    ok = [v for v in per_round if v is not None]
     return dict(bytes=HBV3_BYTES, iters=HBV3_ITERS, round_aggregate_GBps=per_round,
-                mean_aggregate_GBps=round(statistics.mean(per_round), 2))
+                mean_aggregate_GBps=round(statistics.mean(ok), 2) if len(ok) == len(per_round) else None)
 
 
-def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
+def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
     """8 B ping-pong half round trip of every pair, round by round
     (PAIR_LATENCY_ITERS iterations each): "g1>g0" -> us, the pair's slower
     side's wall time / (2 x iterations)."""
@@ -323,7 +349,7 @@ def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
     for rd in range(len(rounds)):
         g, peer = round_role(rounds, rd, rank)
         dist.barrier()
-        walls.append(c.xfer(mpx.MODE_PINGPONG, g, rank, peer, PAIR_LATENCY_ITERS, tx, rx, 8).wall_s)
+        walls.append(safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, PAIR_LATENCY_ITERS, tx, rx, 8))
     mine = torch.tensor(walls, dtype=torch.float64)
     every = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(every, mine)
@@ -333,7 +359,7 @@ def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx) -> dict:
             g, peer = round_role(rounds, rd, r)
             if g == 1:
                 w = max(float(every[r][rd]), float(every[peer][rd]))
-                out[f"{r}>{peer}"] = round(w / (2 * PAIR_LATENCY_ITERS) * 1e6, 3)
+                out[f"{r}>{peer}"] = finite(w / (2 * PAIR_LATENCY_ITERS) * 1e6, 3)
     return dict(sorted(out.items(), key=lambda kv: tuple(int(x) for x in kv[0].split(">"))))
 
 
@@ -406,10 +432,18 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         (nwg, stream), out["push_tune"] = pick_push(torch, dist, tune_times, nbytes)
     out["push"] = push_name(nwg, stream) if nwg else "default"
 
+    step_err = []
+
     def step(s: int):
         g, peer = round_role(rounds, s % len(rounds), rank)
         dist.barrier()                               # MPI_Barrier, mpi_perf.c:499
-        return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream)
+        if step_err:                                 # keep joining the barriers, transfer nothing
+            return g, None
+        try:
+            return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream)
+        except Exception as e:  # noqa: BLE001
+            step_err.append(f"rank {rank}: step {s}: {type(e).__name__}: {e}"[:300])
+            return g, None
 
     for s in range(warmup):
         step(s)
@@ -419,6 +453,8 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     t0 = time.perf_counter()
     for s in range(steps):
         g, t = step(s)
+        if t is None:
+            continue
         step_wall[s] = t.wall_s
         if g == 1:
             dev_s += t.device_s
@@ -426,6 +462,11 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
             step_dev[s] = t.device_s
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    err = agree(step_err[0] if step_err else "")
+    if err:   # a timed step failed on some rank: no headline from this engine
+        c.close()
+        dist.barrier()
+        return {"error": err}
     tt = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     out["elapsed"] = float(tt[0])
@@ -436,16 +477,22 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     out["per_pair_GBps"] = nbytes * iters / out["per_launch_s"] / 1e9
     out.update(pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, nbytes * iters))
     if latency:
+        # after the headline: a failure here costs its own numbers only
+        errs = []
         g, peer = round_role(rounds, 0, rank)
         dist.barrier()
-        lt = c.xfer(mpx.MODE_PINGPONG, g, rank, peer, LATENCY_ITERS, tx, rx, 8)
-        lat = torch.tensor([lt.wall_s], dtype=torch.float64)
+        lat = torch.tensor([safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, LATENCY_ITERS, tx, rx, 8)],
+                           dtype=torch.float64)
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
-        out["pingpong_8B_half_rtt_us"] = round(float(lat[0]) / (2 * LATENCY_ITERS) * 1e6, 3)
-        out["pair_pingpong_8B_half_rtt_us"] = pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx)
-        out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes)
+        out["pingpong_8B_half_rtt_us"] = finite(float(lat[0]) / (2 * LATENCY_ITERS) * 1e6, 3)
+        out["pair_pingpong_8B_half_rtt_us"] = pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs)
+        out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs)
         if nbytes >= HBV3_BYTES:
-            out["hbv3_rounds"] = hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx)
+            out["hbv3_rounds"] = hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs)
+        every = [None] * world
+        dist.all_gather_object(every, errs[:3])
+        if any(every):
+            out["extras_errors"] = {str(r): e for r, e in enumerate(every) if e}
     dist.barrier()
     c.close()
     dist.barrier()   # see above: all imports closed before the next allocation
@@ -455,8 +502,9 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
 def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
                         extras: dict) -> tuple[dict, str]:
     """pairs_bench on `engine`; if the kernel engine fails (payload
-    validation or a device timeout on any rank), measure the SDMA engine
-    instead and say so: an explicit, labelled fallback, never a silent one."""
+    validation, or a device timeout on any rank in validation or in the timed
+    steps), measure the SDMA engine instead and say so: an explicit, labelled
+    fallback, never a silent one."""
     res = pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync)
     engine_used = engine
     if res.get("error") and engine == "kernel":
@@ -467,7 +515,7 @@ def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iter
             fb = pairs_bench(mpx, torch, dist, fb_engine, rank, world, dev, nbytes, iters, steps, warmup,
                              barrier_sync)
             if not fb.get("error"):
-                res, engine_used = fb, f"{fb_engine} (fallback: kernel engine failed validation)"
+                res, engine_used = fb, f"{fb_engine} (fallback: kernel engine failed, extras.kernel_engine_error)"
                 break
             extras[f"{fb_engine}_engine_error"] = fb["error"]
     if res.get("error"):
@@ -631,6 +679,8 @@ def main() -> None:
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
             extras["pair_pingpong_8B_half_rtt_us"] = res["pair_pingpong_8B_half_rtt_us"]
+        if "extras_errors" in res:
+            extras["pair_extras_errors"] = res["extras_errors"]
         if "hbv3_rounds" in res:
             extras["hbv3_rounds_unidir"] = res["hbv3_rounds"]
         if "round0_sweep" in res:

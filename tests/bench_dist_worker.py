@@ -91,6 +91,11 @@ class FakeMpx:
                  timeout_ms=0, nwg=0, stream=False):
             if check_payload and self.engine == "kernel" and scenario == "kernel_fails_validation" and rank == 0:
                 raise FakeError("payload checksum mismatch")
+            if (scenario == "kernel_step_fails" and self.engine == "kernel" and rank == 1 and mode == 2 and
+                    not check_payload and iters == 500):
+                raise FakeError("device-side wait timed out (timed step)")
+            if scenario == "latency_fails" and rank == 1 and mode == 0 and n == 8:
+                raise FakeError("device-side wait timed out (LL ping-pong)")
             FakeMpx.log.append(["xfer", self.engine, mode, group, me, peer, iters, n, bool(check_payload), expect,
                                 expect_ack, nwg, stream])
             time.sleep(0.002)

@@ -97,3 +97,32 @@ def test_hbv3_shaped_rounds():
     assert h["bytes"] == 456131 and h["iters"] == 10 and len(h["round_aggregate_GBps"]) == 3
     # the stand-in's wall time is 2 ms: 2 pairs x 456131 B x 10 / 2 ms
     assert all(abs(v - 2 * 456131 * 10 / 0.002 / 1e9) < 0.05 for v in h["round_aggregate_GBps"])
+
+
+def test_failure_after_the_headline_keeps_the_line():
+    """Rank 1's 8 B ping-pong fails (a device deadline) after the timed steps:
+    every rank still runs every later collective, the headline and the other
+    extras stand, and the failed numbers are null with the error reported."""
+    rcs, outs = run("latency_fails")
+    assert rcs == [0, 0], [o[1][-600:] for o in outs]
+    d = lines(outs[0][0])[0]
+    e = d["extras"]
+    assert d["value"] > 0 and d["config"]["engine"] == "kernel"
+    assert e["pingpong_8B_half_rtt_us"] is None
+    assert all(v is None for v in e["pair_pingpong_8B_half_rtt_us"].values())
+    assert "LL ping-pong" in e["pair_extras_errors"]["1"][0]
+    assert e["round0_sweep"]["unidir_4194304"]["GBps"] > 0
+    assert isinstance(e["sdma_aggregate_GBps"], float)
+    json.dumps(d, allow_nan=False)          # strict JSON: no Infinity / NaN
+
+
+def test_failed_timed_step_falls_back_to_sdma_with_a_label():
+    """Rank 1's kernel-engine transfer fails inside the timed steps: rank 0
+    keeps joining the step barriers, both agree on the error afterwards, and
+    the SDMA engine carries the line, labelled, with the kernel error kept."""
+    rcs, outs = run("kernel_step_fails")
+    assert rcs == [0, 0], [o[1][-600:] for o in outs]
+    d = lines(outs[0][0])[0]
+    assert d["config"]["engine"].startswith("sdma (fallback")
+    assert "timed step" in d["extras"]["kernel_engine_error"] and "rank 1" in d["extras"]["kernel_engine_error"]
+    assert d["value"] > 0
