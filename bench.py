@@ -177,15 +177,16 @@ def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: in
 POST_TIMEOUT_MS = 2000
 
 
-def safe_wall(c, errs: list, *xfer_args) -> float:
+def safe_wall(c, errs: list, *xfer_args, **xfer_kw) -> float:
     """Wall time of one transfer measured after the headline (latency,
-    sweeps); a failure there (a device deadline, a refused transfer) is
-    recorded in `errs` and returns +inf, so this rank still takes part in
-    every collective that follows and the headline line is still printed."""
+    sweeps); a failure there (a device deadline, a refused transfer, a
+    payload checksum mismatch) is recorded in `errs` and returns +inf, so
+    this rank still takes part in every collective that follows and the
+    headline line is still printed."""
     try:
         # a 2 s per-wait deadline (the longest wait here is one 4 MiB push):
         # a broken link costs each later partner 2 s, not the default 10
-        return c.xfer(*xfer_args, timeout_ms=POST_TIMEOUT_MS).wall_s
+        return c.xfer(*xfer_args, timeout_ms=POST_TIMEOUT_MS, **xfer_kw).wall_s
     except Exception as e:  # noqa: BLE001
         errs.append(f"{type(e).__name__}: {e}"[:240])
         return float("inf")
@@ -312,6 +313,33 @@ def pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, lau
 
 
 PAIR_LATENCY_ITERS = 10_000
+# small messages checked on every link before they are timed: the LL protocol
+# (<= 8 KiB across xGMI) and the first bulk size above it; validation of the
+# headline covers only B
+SMALL_CHECK_SIZES, SMALL_CHECK_ITERS = (1, 8, 4097, 8192, 8193), 20
+
+
+def small_message_check(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes, errs) -> dict:
+    """Ping-pong with every received payload checksummed (check mode) at
+    SMALL_CHECK_SIZES on every round's pairs, i.e. on every link the steps
+    used: the small-message protocol's payloads are verified on the node's
+    own links, beside the latency they are timed at."""
+    sizes = [n for n in SMALL_CHECK_SIZES if n <= nbytes]
+    mine = [c.checksum(tx, n) for n in sizes]
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    before = len(errs)
+    for rd in range(len(rounds)):
+        g, peer = round_role(rounds, rd, rank)
+        for k, n in enumerate(sizes):
+            dist.barrier()
+            safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, SMALL_CHECK_ITERS, tx, rx, n,
+                      check_payload=True, expect=every[peer][k])
+    bad = torch.tensor([float(len(errs) - before)], dtype=torch.float64)
+    dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+    return dict(sizes=sizes, iters=SMALL_CHECK_ITERS, rounds=len(rounds),
+                payloads_checked=world * len(rounds) * len(sizes) * SMALL_CHECK_ITERS,
+                failed_transfers=int(bad[0]))
 # BASELINE config 4's other workload, scripts/run-hbv3.sh: -u 1 -b 456131 -i 10
 HBV3_BYTES, HBV3_ITERS, HBV3_PASSES = 456131, 10, 3
 
@@ -396,8 +424,11 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     if engine == "rccl" and not err:
         uid = [mpx.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-    # phase 2: map the peers, validate every round once (collectives only
-    # between the phases: each pair synchronises itself inside xfer)
+    # phase 2: map the peers, then validate every round once, each round
+    # behind a barrier like a reference run (mpi_perf.c:499); a rank whose
+    # transfer failed keeps joining the barriers, so no rank is left inside a
+    # collective; the push tuning has no collectives (each pair synchronises
+    # itself inside xfer)
     if not err:
         try:
             for r in range(world):
@@ -405,15 +436,27 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
                     c.import_rank(r, descs[r][0])
             if engine == "rccl":
                 c.rccl_init_rank(rank, world, uid[0])
-            for r in range(len(rounds)):
-                g, peer = round_role(rounds, r, rank)
-                c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True,
-                       expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000)
-            if engine == "kernel" and tune:
-                tune_times = tune_push_local(mpx, c, rounds, rank, world, tx, rx, nbytes, [d[1] for d in descs],
-                                             [d[2] for d in descs])
         except Exception as e:  # noqa: BLE001
             err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
+        err = agree(err)
+    if not err:
+        for r in range(len(rounds)):
+            g, peer = round_role(rounds, r, rank)
+            dist.barrier()
+            if err:
+                continue
+            try:
+                c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True,
+                       expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {rank}: round {r}: {type(e).__name__}: {e}"[:300]
+        err = agree(err)
+    if not err and engine == "kernel" and tune:
+        try:
+            tune_times = tune_push_local(mpx, c, rounds, rank, world, tx, rx, nbytes, [d[1] for d in descs],
+                                         [d[2] for d in descs])
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {rank}: push tuning: {type(e).__name__}: {e}"[:300]
         err = agree(err)
     if err:
         if c is not None:
@@ -479,6 +522,8 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     if latency:
         # after the headline: a failure here costs its own numbers only
         errs = []
+        out["small_message_check"] = small_message_check(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes,
+                                                         errs)
         g, peer = round_role(rounds, 0, rank)
         dist.barrier()
         lat = torch.tensor([safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, LATENCY_ITERS, tx, rx, 8)],
@@ -681,6 +726,8 @@ def main() -> None:
             extras["pair_pingpong_8B_half_rtt_us"] = res["pair_pingpong_8B_half_rtt_us"]
         if "extras_errors" in res:
             extras["pair_extras_errors"] = res["extras_errors"]
+        if "small_message_check" in res:
+            extras["small_message_check"] = res["small_message_check"]
         if "hbv3_rounds" in res:
             extras["hbv3_rounds_unidir"] = res["hbv3_rounds"]
         if "round0_sweep" in res:

@@ -53,7 +53,7 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         imports = sorted(x[1] for x in d["log"] if x[0] == "import")
         assert imports == [q for q in range(world) if q != r]
         xf = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel"]
-        checked = [x for x in xf if x[8]]
+        checked = [x for x in xf if x[8] and x[2] == 2]
         timed = [x for x in xf if not x[8] and x[2] == 2][:warmup + steps]
         # validation: one checked transfer per round, against the PEER's tx
         assert len(checked) == world - 1
@@ -62,6 +62,17 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
             assert (x[3], x[4], x[5], x[6], x[7]) == (g, r, peer, 3, n)
             assert x[9] == (key(peer) * 31 + n) & 0xFFFFFFFFFFFFFFFF
             assert x[10] == (key(peer) * 31 + 1) & 0xFFFFFFFFFFFFFFFF
+        # after the headline: checked ping-pong at the small sizes <= B on
+        # every round, each against the peer's tx prefix of that size
+        small = [x for x in xf if x[8] and x[2] == 0]
+        sizes = [1, 8]                                        # SMALL_CHECK_SIZES <= B = 4096
+        assert len(small) == (world - 1) * len(sizes)
+        for i, x in enumerate(small):
+            g, peer = round_role(rounds, i // len(sizes), r)
+            m = sizes[i % len(sizes)]
+            assert (x[3], x[5], x[6], x[7]) == (g, peer, 20, m)
+            assert x[9] == (key(peer) * 31 + m) & 0xFFFFFFFFFFFFFFFF
+        assert d["res"]["small_message_check"]["failed_transfers"] == 0
         # warmup + timed steps: step s runs round s mod (N-1)
         assert len(timed) == warmup + steps
         for s, x in enumerate(timed):
@@ -77,7 +88,7 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
     # then every round's pairs with 10^4, then the round-0 size sweep (config 3: unidir and full-duplex -x 1)
     for d in res:
         r = d["rank"]
-        pp = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0]
+        pp = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0 and not x[8]]
         assert len(pp) == world and pp[0][6] == 100_000 and pp[0][7] == 8
         # then 10^4 iterations of 8 B on every round: every pair's latency
         for rd, x in enumerate(pp[1:]):
