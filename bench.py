@@ -16,12 +16,18 @@ A "step" is one run of the reference's loop (mpi_perf.c:474-569: barrier ->
   with the 1-byte ack (mpi_perf.c:127-145).  value = sum of bytes over all
   pairs / T, with T the max over ranks (weak scaling: every GPU is in one
   pair per step).  Before the timed steps every round is validated once
-  (check mode, seeded payloads) and the bulk push variant (workgroups per
-  push x streaming store hint) is tuned on round 0's links; after them come
-  the 8 B latency (10^5 ping-pong iterations), config 3's pair sweep, and the
-  SDMA and RCCL comparison engines under a watchdog.
+  (check mode, seeded payloads, a barrier per round) and the bulk push
+  variant (workgroups per push x streaming store hint) is tuned on round 0's
+  links.  After them come the per-pair table of every covered pair, a
+  checked small-message ping-pong on every link, the 8 B latency (10^5
+  ping-pong iterations on round 0, 10^4 on every pair), config 3's pair
+  sweep, run-hbv3's 456131 B x 10 rounds, and the SDMA and RCCL comparison
+  engines under a watchdog.  A kernel-engine failure before or inside the
+  timed steps falls back to SDMA (labelled); a failure after them nulls only
+  its own numbers.
 
-Rank 0 prints one JSON line.  `roofline` is computed for the dominant kernel
+Rank 0 prints one JSON line, and it is the only thing on stdout (library
+output on fd 1 is routed to stderr).  `roofline` is computed for the dominant kernel
 from HIP-event time measured inside this process (libmpx records the events
 on the stream it launches on); `cpu_baseline` times the compiled reference
 (oracle/_ref, under MPICH shared memory) or, if absent, the oracle's CPU port.
