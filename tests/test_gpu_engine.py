@@ -196,8 +196,23 @@ def test_sdma_graph_chunks_keep_sequence_state(mode):
         P.close()
 
 
-@pytest.mark.parametrize("name", ["pingpong_p2_b456131_i3", "unidir_p2_b4096_i7", "pingpong_p4_b8_i10",
-                                  "unidir_p4_b456131_i3", "nonblocking_p2_b4096_i7", "defaults_unidir"])
+def _digest_cases():
+    """Every golden run that transfers data in the -p layout (ranks [0, p) in
+    group 1, rank k paired with p + k): all mode x ppn x size cases, the
+    non-blocking window quirk, defaults, 0 bytes, 0 iterations, 0 runs, -u 1
+    over -x 1, the 1002-run summary case and the 2^31 - 1-byte buffer."""
+    out = []
+    for c in O.golden()["cases"]:
+        a = c["args"]
+        if c.get("returncode") or not c.get("shim") or "-d" in a or c["np"] != 2 * c["ppn"]:
+            continue
+        if a[a.index("-n") + 1] != "1":
+            continue
+        out.append(c["name"])
+    return out
+
+
+@pytest.mark.parametrize("name", _digest_cases())
 def test_receive_digest_matches_reference(name):
     """Runs the golden case's configuration (pairs, mode, B, iters, runs) on the
     GPU with every payload checksummed, and compares each rank's receive
