@@ -212,8 +212,9 @@ def _digest_cases():
     return out
 
 
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
 @pytest.mark.parametrize("name", _digest_cases())
-def test_receive_digest_matches_reference(name):
+def test_receive_digest_matches_reference(name, engine):
     """Runs the golden case's configuration (pairs, mode, B, iters, runs) on the
     GPU with every payload checksummed, and compares each rank's receive
     digest with what the compiled reference's ranks received."""
@@ -224,7 +225,7 @@ def test_receive_digest_matches_reference(name):
     iters = int(a[a.index("-i") + 1]) if "-i" in a else 10
     B = int(a[a.index("-b") + 1]) if "-b" in a else 456131
     mode = mpx.MODE_UNIDIR if "-u" in a else (mpx.MODE_NONBLOCKING if "-x" in a else mpx.MODE_PINGPONG)
-    P = Pairs("kernel", ppn, max(B, 1))
+    P = Pairs(engine, ppn, max(B, 1))
     try:
         digest = {r: [0, 0, 0] for r in range(2 * ppn)}
         for _ in range(runs):
