@@ -32,13 +32,20 @@ def run(tmp_path, args, lines=("vm",), names="vm,runsc", gpus="0,0"):
     return p, recs, side
 
 
-@pytest.mark.parametrize("name", ["pingpong_p1_b456131_i3", "unidir_p2_b4096_i7", "nonblocking_p2_b8_i10",
-                                  "unidir_p1_b8_i10", "pingpong_p2_b1_i10"])
+def _record_cases():
+    """every golden run that moves data in the -p layout with one -f line"""
+    return [c["name"] for c in O.golden()["cases"]
+            if not c.get("returncode") and c.get("shim") and "-d" not in c["args"] and c["np"] == 2 * c["ppn"]
+            and c["args"][c["args"].index("-n") + 1] == "1"]
+
+
+@pytest.mark.parametrize("name", _record_cases())
 def test_records_match_reference_run(tmp_path, name):
     c = GOLDEN[name]
-    names = ",".join(["vm"] * c["ppn"] + ["runsc"] * c["ppn"])
+    names = ",".join([c["host1"]] * c["ppn"] + [c["host0"]] * c["ppn"])
     gpus = ",".join(["0"] * c["np"])
-    p, recs, side = run(tmp_path, ["-w", str(c["np"])] + c["args"] + ["-c", "1"], names=names, gpus=gpus)
+    p, recs, side = run(tmp_path, ["-w", str(c["np"])] + c["args"] + ["-c", "1"], lines=c["group1_lines"],
+                        names=names, gpus=gpus)
     assert p.returncode == 0, p.stderr[-600:]
     assert len(recs) == c["n_records"]
     ref = sorted((r["rank"], r["vmcount"], r["flows"], r["buffer_size"], r["num_buffers"], r["run_id"])
