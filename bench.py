@@ -116,6 +116,27 @@ def traffic_from_profile(workload: str) -> dict | None:
         return json.load(f)
 
 
+def copy_sweep(mpx, c, src, dst, nbytes: int) -> dict:
+    """BASELINE config 2's sweep beside the headline: k_copy at B = 2^k for
+    1 B .. nbytes.  Each size: 10 back-to-back launches (3 at >= 256 MiB)
+    timed together with HIP events on the copy's stream, best of 5 such
+    batches (tools/copy_sweep.py's method); HBM traffic 2B per launch over
+    the average launch time.  Small sizes are launch-bound; the output of the
+    last size is checked."""
+    best = {}
+    for _ in range(2):   # two passes over the sizes: a clock transition mid-pass costs one pass only
+        b = 1
+        while b <= nbytes:
+            launches = 10 if b < (256 << 20) else 3
+            c.copy(0, dst, src, b, 2)   # warm: first launches of this grid size
+            per = min(t.device_s / max(t.launches, 1) for t in (c.copy(0, dst, src, b, launches) for _ in range(5)))
+            best[b] = min(best.get(b, per), per)
+            b *= 2
+    out = {str(k): dict(us=round(v * 1e6, 2), hbm_GBps=round(2 * k / v / 1e9, 1)) for k, v in sorted(best.items())}
+    assert c.checksum(dst, b // 2) == c.checksum(src, b // 2), "copy sweep output differs from its input"
+    return out
+
+
 def hbm_one_direction_ceiling() -> dict | None:
     """Read-only and write-only HBM rates of k_copy's access shape (one 16-B
     nontemporal unit per lane, one step per workgroup), measured by
@@ -688,6 +709,7 @@ def main() -> None:
                       parallelism="single GPU")
         metric_unit = "GB/s"
         if not args.no_extras:
+            extras["copy_sweep"] = copy_sweep(mpx, c, src, dst, nbytes)
             lat = loopback_pair(mpx, "kernel", mpx.MODE_PINGPONG, 8, 5000)
             extras["loopback_pingpong_8B_half_rtt_us"] = round(lat["per_iter_us"] / 2, 3)
             uni = loopback_pair(mpx, "kernel", mpx.MODE_UNIDIR, 4 << 20, 200)
