@@ -809,6 +809,8 @@ def main() -> None:
             r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
                              latency=False)
             extras[f"{eng}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
+            # every round's payloads checksummed on this engine before timing (BASELINE config 5)
+            extras[f"{eng}_validated_rounds"] = r2.get("validated_rounds", 0)
         with lock:
             done.set()
         dog.cancel()

@@ -49,6 +49,8 @@ def test_one_json_line_with_the_contract_keys():
     assert d["roofline"]["bound"] == "xgmi" and d["roofline"]["peak"] == 76.8
     assert isinstance(d["extras"]["sdma_aggregate_GBps"], float)
     assert isinstance(d["extras"]["rccl_aggregate_GBps"], float)
+    # the comparison engines checksum every round before timing it (config 5)
+    assert d["extras"]["sdma_validated_rounds"] == 1 and d["extras"]["rccl_validated_rounds"] == 1
 
 
 def test_hung_comparison_engine_cannot_cost_the_line():
