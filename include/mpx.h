@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 1
+#define MPX_ABI_VERSION 2
 #define MPX_MAX_RANKS 16          /* ranks one context can address           */
 #define MPX_RANK_DESC_BYTES 512   /* size of the opaque exported descriptor  */
 #define MPX_RCCL_ID_BYTES 128     /* size of an RCCL unique id               */
@@ -103,6 +103,15 @@ typedef struct mpx_timing {
                                  3 = RCCL, 4 = local copy kernel               */
     int32_t check_failures;   /* iterations whose payload checksum mismatched  */
     uint64_t check_iters;     /* iterations whose payload was checksummed      */
+    /* receive accounting, as the reference's loop completes receives: every
+       Recv of ping-pong / unidir (mpi_perf.c:75,79,137,141), and the requests
+       each MPI_Waitall of the non-blocking loop waits for (:110-111,122-123;
+       slot 255 of each full window is never waited for).  Counted on the
+       device (kernel engine always; SDMA / RCCL engines in check mode). */
+    uint64_t recv_done;       /* receives completed                             */
+    uint64_t recv_digest;     /* check mode: sum of mpx_checksum() of each of
+                                 those received payloads (the golden fixtures'
+                                 recv_digest); 0 otherwise                      */
 } mpx_timing;
 
 /* options of mpx_xfer_ex beyond the reference seam */

@@ -23,16 +23,21 @@ constexpr int kStageMaxBytes = 60 << 10; // LDS-staged tx chunk per workgroup, m
 enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4 };
 
 // One rank's receive mailbox, in that rank's HBM (uncached / fine-grained so a
-// poll sees stores that arrive over xGMI).  Written ONLY by senders, polled
+// poll sees stores that arrive over xGMI).  Written ONLY by the peers, polled
 // only by the owner.
-//   flag[s][w] : sequence number of the last bulk push workgroup w of sender
-//                rank s finished into this rank's rx (written with one
-//                system-scope store after that workgroup's payload drained)
-//   ll[s][g]   : LL granule g of the current small message from sender s:
-//                {tag:32 | payload:32}, tag = ll_tag(seq), one 8-byte store
+//   flag[s][w]   : sequence number of the last bulk push workgroup w of sender
+//                  rank s finished into this rank's rx (written with one
+//                  system-scope store after that workgroup's payload drained)
+//   ll[s][g]     : LL granule g of the current small message from sender s:
+//                  {tag:32 | payload:32}, tag = ll_tag(seq), one 8-byte store
+//   credit[s][w] : non-blocking check mode only — sequence number of the last
+//                  of THIS rank's pushes whose chunk w rank s has checksummed
+//                  (and poisoned), i.e. the ring slot it used is free again;
+//                  rx_seq0 at the start of each of s's checked calls
 struct Mailbox {
     u64 flag[MPX_MAX_RANKS][kMaxPushWG];
     u64 ll[MPX_MAX_RANKS][kLLGranules];
+    u64 credit[MPX_MAX_RANKS][kMaxPushWG];
 };
 
 // Per-rank host-mapped status words (written by the device, read by the host
@@ -41,7 +46,30 @@ struct Status {
     unsigned int err;       // bit0: a wait timed out
     unsigned int where;     // 1 + iteration index of the first timeout
     u64 spins;              // diagnostics: polls of the last wait
+    // receive accounting of the last call, counted on the device where the
+    // reference's call returns a receive (Recv, or Waitall for the
+    // non-blocking loop, mpi_perf.c:75,79,110-111,122-123,137,141)
+    u64 recv_done;          // receives completed
+    u64 recv_digest;        // check mode: sum of their finished checksums
 };
+
+// Device scratch words of a rank (zeroed per kernel-engine call, [0..3]):
+//   [0] grid-barrier counter  [1] abort word  [2] finished workgroups
+//   [4..5] SDMA engine's device-side sequence base {tx, rx}
+constexpr int kScratchWords = 8;
+constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrSeqBase = 4;
+
+// Non-blocking check mode ("ring"): receive j of a call with `iters`
+// iterations lands in slot (iters-1-j) mod S of the receiver, where slot 0 is
+// rx itself (so rx ends holding the last payload, as in the reference) and
+// slot s >= 1 is ring + (s-1)*B.  S = min(256, 1 + ring_bytes / B), computed
+// from the RECEIVER's ring on both sides of the link.
+inline int ring_slots(unsigned long long ring_bytes, long long len) {
+    if (len <= 0) return kNbWindow;
+    const unsigned long long s = 1 + ring_bytes / (unsigned long long)len;
+    return s < (unsigned long long)kNbWindow ? (int)s : kNbWindow;
+}
+__host__ __device__ inline int ring_slot(int j, int iters, int slots) { return (iters - 1 - j) % slots; }
 
 // Arguments of one transfer loop on one rank (kernel engine).
 struct XferArgs {
@@ -73,6 +101,13 @@ struct XferArgs {
                                  // pushes (divides kNbWindow) and at the last
     int stage;                   // bytes of dynamic LDS holding this workgroup's
                                  // chunk of tx (0: bulk pushes read tx from HBM)
+    // non-blocking check mode (k_xfer_nbcheck)
+    unsigned char* ring;         // my receive slots 1..slots-1
+    unsigned char* peer_ring;    // the peer's, mapped here
+    u64* cnt;                    // [iters] workgroups done checking receive j
+    int slots;                   // S: receive slots per link (ring_slots)
+    int skip_push;               // test knob: 1 + iteration whose payload stores
+                                 // are skipped (flag still published); 0 = off
 };
 
 // LL threshold of a link.  Within one GPU the bulk path's extra hop (payload
@@ -111,5 +146,8 @@ hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s)
 hipError_t launch_signal(u64* flag, const u64* base, u64 value, hipStream_t s);
 hipError_t launch_wait(const u64* flag, const u64* base, u64 value, Status* st, u64 timeout_ticks, hipStream_t s);
 hipError_t launch_seqbase(u64* base, u64 tx, u64 rx, int add, hipStream_t s);
+// stream engines' receive accounting: st->recv_done += count and, when csum is
+// set, st->recv_digest += sum_j (csum[j] ^ mix64(n)) over j in [j0, j0+count)
+hipError_t launch_account(Status* st, const u64* csum, int j0, int count, long long n, hipStream_t s);
 
 }  // namespace mpx

@@ -302,15 +302,18 @@ struct Loop {
     }
 
     // publish = false: the stores are issued but not drained and no flag is
-    // stored (non-blocking mode publishes every a.nb_publish pushes, see k_xfer)
-    __device__ void push_bulk(long long n, u64 seq, bool publish = true) const {
+    // stored (non-blocking mode publishes every a.nb_publish pushes, see k_xfer).
+    // dst_base: the peer's receive slot (default: its rx).  skip (test knob
+    // MPX_TEST_SKIP_PUSH): no payload stores, the flag is still published.
+    __device__ void push_bulk(long long n, u64 seq, bool publish = true, unsigned char* dst_base = nullptr,
+                              bool skip = false) const {
         const int w = blockIdx.x;
         if (w >= a.nwg) return;
         long long lo, hi;
         chunk_of(n, &lo, &hi);
-        if (lo < hi) {
+        if (lo < hi && !skip) {
             const unsigned bytes = (unsigned)(hi - lo);
-            const __amdgpu_buffer_rsrc_t dst = rsrc(a.peer_rx + lo, bytes);
+            const __amdgpu_buffer_rsrc_t dst = rsrc((dst_base ? dst_base : a.peer_rx) + lo, bytes);
             const int nv = (int)(bytes >> 4);
             const v4u* src = a.stage ? s_tx : reinterpret_cast<const v4u*>(a.tx + lo);
             if (a.stream) push_units<kAuxSysNt>(src, dst, nv);
@@ -327,8 +330,23 @@ struct Loop {
         if (threadIdx.x == 0) st_sys(&a.peer_mb->flag[a.my_slot][w], seq);
     }
 
-    __device__ void send(long long n, u64 seq) const {
-        if (is_ll(n)) push_ll(n, seq); else push_bulk(n, seq);
+    __device__ void send(long long n, u64 seq, bool skip = false) const {
+        if (is_ll(n)) { if (!skip) push_ll(n, seq); else push_ll_tags_only(n, seq); }
+        else push_bulk(n, seq, true, nullptr, skip);
+    }
+
+    // test knob: an LL message whose payload was "lost" — the tags arrive (so
+    // the receiver completes), the data words carry a fixed wrong pattern
+    __device__ void push_ll_tags_only(long long n, u64 seq) const {
+        if (blockIdx.x != 0) return;
+        const int ng = n > 0 ? (int)((n + 3) >> 2) : 1;
+        const int nu = (ng + 1) >> 1;
+        const unsigned tag = ll_tag(seq);
+        const __amdgpu_buffer_rsrc_t dst = rsrc(&a.peer_mb->ll[a.my_slot][0], (unsigned)(nu * 16));
+        for (int u = threadIdx.x; u < nu; u += kBlock) {
+            const v4u v = {~0u, tag, ~0u, tag};
+            __builtin_amdgcn_raw_buffer_store_b128(v, dst, (unsigned)u * 16, 0, kAuxSys);
+        }
     }
 
     // ---- receive: wait until the peer's push `seq` of n bytes has landed ----
@@ -424,43 +442,151 @@ struct Loop {
                     for (long long o = threadIdx.x; o < n; o += kBlock) a.rx[o] = (unsigned char)poison;
             }
         } else if ((int)blockIdx.x < a.nwg) {
-            // bytes stored by the peer: system-scope acquire, then sc0|sc1 loads
-            if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            drain_stores();
-            __syncthreads();
-            const long long chunk = (((n + a.nwg - 1) / a.nwg) + 15) & ~15ll;
-            const long long lo = (long long)blockIdx.x * chunk;
-            const long long hi = lo + chunk < n ? lo + chunk : n;
-            if (lo < hi) {
-                const unsigned bytes = (unsigned)(hi - lo);
-                const __amdgpu_buffer_rsrc_t r = rsrc(a.rx + lo, bytes);
-                const int nv = (int)(bytes >> 4);
-                const v4u pv = {(unsigned)poison, (unsigned)(poison >> 32), (unsigned)poison, (unsigned)(poison >> 32)};
-                for (int v = threadIdx.x; v < nv; v += kBlock) {
-                    const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, v * 16, 0, kAuxSys);
-                    const u64 k = (u64)(lo / 8) + 2 * (u64)v;
-                    acc += csum_term(((u64)x.y << 32) | x.x, k);
-                    acc += csum_term(((u64)x.w << 32) | x.z, k + 1);
-                    if (!last) __builtin_amdgcn_raw_buffer_store_b128(pv, r, v * 16, 0, kAuxSys);
-                }
-                const unsigned tail = bytes & 15;   // only the last workgroup
-                if (threadIdx.x < 2 && 8 * threadIdx.x < tail) {
-                    const long long off = lo + (long long)nv * 16 + 8 * threadIdx.x;
-                    u64 w = 0;
-                    for (long long b = 0; b < 8 && off + b < n; ++b) {
-                        const unsigned char c = __builtin_amdgcn_raw_buffer_load_b8(r, (unsigned)(off - lo + b), 0, kAuxSys);
-                        w |= (u64)c << (8 * b);
-                    }
-                    acc += csum_term(w, (u64)off / 8);
-                }
-                __syncthreads();
-                if (!last && threadIdx.x < tail)
-                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)poison, r, (unsigned)nv * 16 + threadIdx.x, 0, kAuxSys);
-            }
-            drain_stores();
+            acc = sum_chunk(a.rx, n, poison, last);
         }
         const u64 s = block_sum(acc, lds4);
         if (threadIdx.x == 0 && s) atomicAdd(&a.csum[iter], s);
+    }
+
+    // This workgroup's chunk of a bulk payload of n bytes at `base` that the
+    // peer stored: system-scope acquire, sc0|sc1 loads, the lane's partial
+    // checksum returned; then poison stores (write-through) unless `keep`,
+    // drained before returning.
+    __device__ u64 sum_chunk(unsigned char* base, long long n, u64 poison, bool keep) const {
+        u64 acc = 0;
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        drain_stores();
+        __syncthreads();
+        long long lo, hi;
+        chunk_of(n, &lo, &hi);
+        if (lo < hi) {
+            const unsigned bytes = (unsigned)(hi - lo);
+            const __amdgpu_buffer_rsrc_t r = rsrc(base + lo, bytes);
+            const int nv = (int)(bytes >> 4);
+            const v4u pv = {(unsigned)poison, (unsigned)(poison >> 32), (unsigned)poison, (unsigned)(poison >> 32)};
+            for (int v = threadIdx.x; v < nv; v += kBlock) {
+                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, v * 16, 0, kAuxSys);
+                const u64 k = (u64)(lo / 8) + 2 * (u64)v;
+                acc += csum_term(((u64)x.y << 32) | x.x, k);
+                acc += csum_term(((u64)x.w << 32) | x.z, k + 1);
+                if (!keep) __builtin_amdgcn_raw_buffer_store_b128(pv, r, v * 16, 0, kAuxSys);
+            }
+            const unsigned tail = bytes & 15;   // only the last workgroup
+            if (threadIdx.x < 2 && 8 * threadIdx.x < tail) {
+                const long long off = lo + (long long)nv * 16 + 8 * threadIdx.x;
+                u64 w = 0;
+                for (long long b = 0; b < 8 && off + b < n; ++b) {
+                    const unsigned char c = __builtin_amdgcn_raw_buffer_load_b8(r, (unsigned)(off - lo + b), 0, kAuxSys);
+                    w |= (u64)c << (8 * b);
+                }
+                acc += csum_term(w, (u64)off / 8);
+            }
+            __syncthreads();
+            if (!keep && threadIdx.x < tail)
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)poison, r, (unsigned)nv * 16 + threadIdx.x, 0, kAuxSys);
+        }
+        drain_stores();
+        return acc;
+    }
+
+    // ---- receive accounting ------------------------------------------------
+    // Ping-pong / unidir: every receive is counted when it completes (a
+    // blocking Recv).  At the end the last workgroup to finish (all chunk
+    // checksums are in by then) adds up the finished checksums of the `done`
+    // receives (check mode) and stores the count and digest.
+    __device__ void account_all(u64 done, long long n_recv) const {
+        __shared__ int s_last;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            s_last = __hip_atomic_fetch_add(&a.gbar[kScrFin], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (u64)gridDim.x - 1;
+        __syncthreads();
+        if (!s_last) return;
+        u64 part = 0;
+        if (a.check) {
+            const u64 fmix = mix64((u64)n_recv);
+            for (u64 j = threadIdx.x; j < done; j += kBlock)
+                part += __hip_atomic_load(&a.csum[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ fmix;
+        }
+        const u64 s = block_sum(part, lds4);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&a.status->recv_digest, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+
+    // ---- non-blocking check mode (k_xfer_nbcheck) ----------------------------
+    // receive slot j of the rank whose rx / ring these are (ring_slot)
+    __device__ unsigned char* slot_base(unsigned char* rx0, unsigned char* ring0, int j) const {
+        const int s = ring_slot(j, a.iters, a.slots);
+        return s == 0 ? rx0 : ring0 + (long long)(s - 1) * a.len;
+    }
+
+    // Check this workgroup's chunk of receive j: checksum + poison its slot
+    // (the last receive stays in rx unpoisoned), add the chunk sum into
+    // csum[j], count the chunk in cnt[j], then hand the slot back to the
+    // sender (credit) — after the poison stores drained, so none can land on
+    // the next payload.
+    __device__ void check_nb(int j) const {
+        const long long n = a.len;
+        const u64 poison = 0x5a5a5a5a5a5a5a5aull ^ (u64)j;
+        const u64 acc = sum_chunk(slot_base(a.rx, a.ring, j), n, poison, j + 1 == a.iters);
+        const u64 s = block_sum(acc, lds4);
+        if (threadIdx.x == 0) {
+            if (s) atomicAdd(&a.csum[j], s);
+            __hip_atomic_fetch_add(&a.cnt[j], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            st_sys(&a.peer_mb->credit[a.my_slot][blockIdx.x], a.rx_seq0 + (u64)j + 1);
+        }
+    }
+
+    // Wait until ready() holds (evaluated by every lane, all must agree),
+    // checking — in order — every receive of this workgroup's chunk that
+    // lands meanwhile.  Both sides do this whenever they wait, so a sender
+    // waiting for a free slot never starves the receiver that must free it.
+    template <class Ready>
+    __device__ bool nb_wait(Ready ready, int* next, int iter) const {
+        u64 t0 = now_ticks(), spins = 0;
+        for (;;) {
+            if (__syncthreads_and(ready())) return true;
+            const bool landed = __syncthreads_or(
+                threadIdx.x == 0 && *next < a.iters &&
+                ld_sys(&a.my_mb->flag[a.peer_slot][blockIdx.x]) >= a.rx_seq0 + (u64)*next + 1);
+            if (landed) {
+                check_nb(*next);
+                ++*next;
+                t0 = now_ticks();
+                continue;
+            }
+            if (__syncthreads_or(threadIdx.x == 0 && should_stop(++spins, t0))) {
+                if (threadIdx.x == 0) give_up(iter);
+                __syncthreads();
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+
+    // Waitall over receives [lo, hi) (workgroup 0): each is complete once
+    // every workgroup has checked its chunk; count them and add their
+    // finished checksums into the digest (thread 0's registers).
+    __device__ bool nb_waitall(int lo, int hi, u64* done, u64* dig, u64 fmix, int* next, int iter) const {
+        const u64 want = (u64)a.nwg;
+        const bool ok = nb_wait(
+            [&] {
+                bool r = true;
+                for (int j = lo + (int)threadIdx.x; j < hi; j += kBlock)
+                    r &= __hip_atomic_load(&a.cnt[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= want;
+                return r;
+            },
+            next, iter);
+        if (!ok) return false;
+        u64 part = 0;
+        for (int j = lo + (int)threadIdx.x; j < hi; j += kBlock)
+            part += __hip_atomic_load(&a.csum[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ fmix;
+        const u64 s = block_sum(part, lds4);
+        *done += (u64)(hi - lo);
+        *dig += s;
+        return true;
     }
 
     // all workgroups finished check(): the 1-WG ack must not overtake a poison
@@ -503,51 +629,140 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     if (ll_send) L.preload_ll(send_len);
     const bool reload = ll_send && (a.ll_flags & 4);   // A/B knob (bit 2): re-read tx at every send
     u64 txs = a.tx_seq0, rxs = a.rx_seq0;
+    u64 done = 0;                                       // receives completed (Status.recv_done)
     int inflight = 0;
     for (int i = 0; i < a.iters; ++i) {
+        const bool skip = a.skip_push == i + 1;        // test knob only
         if constexpr (MODE == MPX_MODE_PINGPONG) {    // mpi_perf.c:70-82
             if constexpr (GROUP == 1) {
                 if (reload) L.preload_ll(send_len);
-                L.send(n, ++txs);                      // Send(tx, B, tag 1)
+                L.send(n, ++txs, skip);                // Send(tx, B, tag 1)
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 2)
+                ++done;
                 if (a.check) L.check(n, i);
             } else {
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 1)
+                ++done;
                 if (a.check) L.check(n, i);
                 if (reload) L.preload_ll(send_len);
-                L.send(n, ++txs);                      // Send(tx, B, tag 2)
+                L.send(n, ++txs, skip);                // Send(tx, B, tag 2)
             }
         } else if constexpr (MODE == MPX_MODE_UNIDIR) {  // mpi_perf.c:132-144
             if constexpr (GROUP == 1) {
                 if (reload) L.preload_ll(send_len);
-                L.send(n, ++txs);                      // Send(tx, B)
+                L.send(n, ++txs, skip);                // Send(tx, B)
                 if (!L.recv(1, ++rxs, i)) break;       // Recv(rx, 1) — the ack
+                ++done;
                 if (a.check) L.check(1, i);
             } else {
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B)
+                ++done;
                 if (a.check) { L.check(n, i); if (!L.grid_sync(i)) break; }
                 if (reload) L.preload_ll(send_len);
-                L.send(1, ++txs);                      // Send(tx, 1)
+                L.send(1, ++txs, skip);                // Send(tx, 1)
             }
         } else {                                       // mpi_perf.c:95-124
             // Isend + Irecv, slot `inflight`.  A receiver waits only at the
             // window flush (i = 255 mod 256) and at the end, so a push needs
             // its drain + flag only every a.nb_publish iterations (a divisor
-            // of 256) and at the last one: the drain's link round trip is
-            // paid once per nb_publish pushes instead of once per push.
-            L.push_bulk(n, ++txs, (i + 1) % a.nb_publish == 0 || i + 1 == a.iters);
+            // of 256), at slot 254 (the last receive a flush waits for) and
+            // at the last one: the drain's link round trip is paid once per
+            // nb_publish pushes instead of once per push, and no flush waits
+            // for the slot-255 push the reference leaves pending.
+            const int slot = i % kNbWindow;
+            L.push_bulk(n, ++txs, (i + 1) % a.nb_publish == 0 || slot == kNbWindow - 2 || i + 1 == a.iters,
+                        nullptr, skip);
             if (inflight == kNbWindow - 1) {
-                // Waitall(255, ...): the receive posted in slot 255 (this
-                // iteration) is not among the 255 waited for (mpi_perf.c:110-111)
+                // Waitall(255, ...): receives of slots 0..254 (iterations
+                // i-255 .. i-1); the receive posted in slot 255 (this
+                // iteration) is not among them (mpi_perf.c:110-111)
                 if (!L.wait_bulk(rxs + i, i)) break;
+                done += (u64)inflight;
                 inflight = 0;
             } else {
                 ++inflight;
             }
         }
     }
-    if constexpr (MODE == MPX_MODE_NONBLOCKING)
-        if (inflight > 0 && !L.aborted()) L.wait_bulk(rxs + a.iters, a.iters - 1);   // final Waitall(inflight)
+    if constexpr (MODE == MPX_MODE_NONBLOCKING) {
+        if (inflight > 0 && !L.aborted() && L.wait_bulk(rxs + a.iters, a.iters - 1))   // final Waitall(inflight)
+            done += (u64)inflight;
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        L.account_all(done, (MODE == MPX_MODE_UNIDIR && GROUP == 1) ? 1 : n);
+    }
+}
+
+// The non-blocking loop in check mode (mpi_perf.c:95-124 with every payload
+// checksummed).  The reference posts up to 256 receives into ONE rx
+// (:100,104); here every receive lands in a slot of its own (ring_slot), so
+// each payload can be checksummed before anything overwrites it.  A sender
+// reuses a slot only after the receiver handed it back (Mailbox.credit);
+// every wait checks the receives that land meanwhile, so neither side can
+// starve the other.  Each workgroup pushes and checks its own chunk.  The
+// windowing is the reference's: Waitall(255) at slot 255 over slots 0..254,
+// the final Waitall(inflight); workgroup 0 counts exactly those receives and
+// digests their checksums.  The receives the reference leaves pending (slot
+// 255 of each full window) are still checked — every payload is — but not
+// counted.  Grid = a.nwg; all workgroups push B bytes.
+__global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
+    __shared__ int s_abort;
+    __shared__ u64 lds4[4];
+    extern __shared__ v4u s_tx[];
+    if (threadIdx.x == 0) s_abort = 0;
+    Loop<MPX_MODE_NONBLOCKING> L{a, &s_abort, lds4, s_tx, {}};
+    const long long n = a.len;
+    if (a.stage) L.stage_tx(n);
+    __syncthreads();
+    const int w = blockIdx.x;
+    // this call starts: every push of the peer before it has been consumed
+    if (threadIdx.x == 0) st_sys(&a.peer_mb->credit[a.my_slot][w], a.rx_seq0);
+    const u64 fmix = mix64((u64)n);
+    const u64* credit = &a.my_mb->credit[a.peer_slot][w];
+    int next = 0, inflight = 0;
+    u64 done = 0, dig = 0;
+    bool ok = true;
+    for (int i = 0; i < a.iters && ok; ++i) {
+        // slot ring_slot(i) was last used by push i - S: wait for its credit
+        // (and, for the first S pushes, for the peer to have started)
+        const u64 want = a.tx_seq0 + (u64)(i >= a.slots ? i - a.slots + 1 : 0);
+        ok = L.nb_wait([&] { return threadIdx.x != 0 || ld_sys(credit) >= want; }, &next, i);
+        if (!ok) break;
+        L.push_bulk(n, a.tx_seq0 + (u64)i + 1, true, L.slot_base(a.peer_rx, a.peer_ring, i), a.skip_push == i + 1);
+        if (inflight == kNbWindow - 1) {               // Waitall(255): iterations i-255 .. i-1
+            ok = L.nb_wait([&] { return next >= i; }, &next, i);
+            if (ok && w == 0) ok = L.nb_waitall(i - inflight, i, &done, &dig, fmix, &next, i);
+            inflight = 0;
+        } else {
+            ++inflight;
+        }
+    }
+    if (ok && inflight > 0) {                          // Waitall(inflight)
+        ok = L.nb_wait([&] { return next >= a.iters; }, &next, a.iters - 1);
+        if (ok && w == 0) ok = L.nb_waitall(a.iters - inflight, a.iters, &done, &dig, fmix, &next, a.iters - 1);
+    }
+    // every payload: also the receives the reference leaves pending
+    if (ok) L.nb_wait([&] { return next >= a.iters; }, &next, a.iters - 1);
+    if (w == 0 && threadIdx.x == 0) {
+        __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.status->recv_digest, dig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// stream engines' receive accounting (launch_account)
+__global__ __launch_bounds__(kBlock) void k_account(Status* st, const u64* csum, int j0, int count, u64 fmix) {
+    __shared__ u64 lds4[4];
+    u64 part = 0;
+    if (csum)
+        for (int j = threadIdx.x; j < count; j += kBlock) part += csum[j0 + j] ^ fmix;
+    const u64 s = block_sum(part, lds4);
+    if (threadIdx.x == 0) {
+        const u64 d = __hip_atomic_load(&st->recv_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const u64 g = __hip_atomic_load(&st->recv_digest, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&st->recv_done, d + (u64)count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&st->recv_digest, g + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -559,7 +774,9 @@ hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
     switch (a.mode) {
         case MPX_MODE_PINGPONG: k = a.group ? k_xfer<MPX_MODE_PINGPONG, 1> : k_xfer<MPX_MODE_PINGPONG, 0>; break;
         case MPX_MODE_UNIDIR: k = a.group ? k_xfer<MPX_MODE_UNIDIR, 1> : k_xfer<MPX_MODE_UNIDIR, 0>; break;
-        case MPX_MODE_NONBLOCKING: k = k_xfer<MPX_MODE_NONBLOCKING, 0>; break;   // both sides alike
+        case MPX_MODE_NONBLOCKING:   // both sides alike
+            k = a.check ? k_xfer_nbcheck : k_xfer<MPX_MODE_NONBLOCKING, 0>;
+            break;
         default: return hipErrorInvalidValue;
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), (unsigned)a.stage, s, a);
@@ -660,6 +877,16 @@ hipError_t launch_wait(const u64* flag, const u64* base, u64 value, Status* st, 
 hipError_t launch_seqbase(u64* base, u64 tx, u64 rx, int add, hipStream_t s) {
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k_seqbase, dim3(1), dim3(64), 0, s, base, tx, rx, add);
+    return hipGetLastError();
+}
+
+hipError_t launch_account(Status* st, const u64* csum, int j0, int count, long long n, hipStream_t s) {
+    const u64 z = (u64)n;
+    u64 m = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;   // mix64(n), host side
+    m = (m ^ (m >> 27)) * 0x94d049bb133111ebull;
+    m ^= m >> 31;
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
+    hipLaunchKernelGGL(k_account, dim3(1), dim3(kBlock), 0, s, st, csum, j0, count, m);
     return hipGetLastError();
 }
 

@@ -106,9 +106,12 @@ struct Rank {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     Status* status = nullptr;      // host-mapped (local ranks)
-    u64* scratch = nullptr;        // [0] grid barrier, [1] abort (local ranks)
-    u64* csum = nullptr;           // per-iteration checksums (device)
+    u64* scratch = nullptr;        // kScratchWords device words (local ranks)
+    u64* csum = nullptr;           // per-iteration checksums (device), csum_cap words,
+    u64* cnt = nullptr;            //   then cnt: checked chunks per receive (csum + csum_cap)
     size_t csum_cap = 0;
+    unsigned char* ring = nullptr; // non-blocking check mode's receive slots 1..S-1
+    uint64_t ring_bytes = 0;
     std::vector<void*> retired;    // outgrown csum arrays (freed at finalize)
     u64 tx_seq[MPX_MAX_RANKS] = {};
     u64 rx_seq[MPX_MAX_RANKS] = {};
@@ -126,6 +129,8 @@ struct RankDesc {
     char host[64];
     hipIpcMemHandle_t rx_handle;
     hipIpcMemHandle_t mb_handle;
+    uint64_t ring_bytes;
+    hipIpcMemHandle_t ring_handle;   // valid when ring_bytes > 0
 };
 static_assert(sizeof(RankDesc) <= MPX_RANK_DESC_BYTES, "rank descriptor too large");
 
@@ -227,12 +232,53 @@ int alloc_mailbox(Rank& rk) {
 int ensure_csum(Rank& rk, int iters) {
     if ((size_t)iters <= rk.csum_cap) return MPX_OK;
     if (rk.csum) rk.retired.push_back(rk.csum);
-    rk.csum = nullptr;
+    rk.csum = rk.cnt = nullptr;
     size_t cap = 1024;
     while (cap < (size_t)iters) cap *= 2;
-    HIPCK(hipMalloc(&rk.csum, cap * sizeof(u64)));
+    HIPCK(hipMalloc(&rk.csum, 2 * cap * sizeof(u64)));
+    rk.cnt = rk.csum + cap;
     rk.csum_cap = cap;
     return MPX_OK;
+}
+
+// Bytes of a rank's check-mode receive ring: up to 255 further slots of the
+// attached length, capped at MPX_CHECK_RING_BYTES (default 64 MiB; 0 = rx
+// only, one slot per link).
+uint64_t ring_bytes_for(size_t len) {
+    static const uint64_t cap = [] {
+        const char* v = getenv("MPX_CHECK_RING_BYTES");
+        return v ? (uint64_t)strtoull(v, nullptr, 0) : (uint64_t)64 << 20;
+    }();
+    if (len == 0) return 0;
+    const uint64_t want = (uint64_t)(kNbWindow - 1) * len;
+    const uint64_t slots = (want < cap ? want : cap) / len;
+    return slots * len;
+}
+
+// receive slots of the link between two ranks: the same on both sides
+int link_slots(const Rank& a, const Rank& b, long long len) {
+    const int sa = ring_slots(a.ring_bytes, len), sb = ring_slots(b.ring_bytes, len);
+    return sa < sb ? sa : sb;
+}
+
+unsigned char* slot_ptr(const Rank& rk, int j, int iters, int slots, long long len) {
+    const int s = ring_slot(j, iters, slots);
+    return s == 0 ? rk.rx : rk.ring + (long long)(s - 1) * len;
+}
+
+// the receives the reference's non-blocking loop completes (Waitall) for
+// `iters` iterations: slot 255 of each full window is never waited for
+// (mpi_perf.c:95-124)
+u64 nb_waited(int iters) {
+    return (u64)iters - (u64)(iters / kNbWindow);
+}
+
+// test knob (MPX_TEST_SKIP_PUSH=k): the k-th push of every call (1-based)
+// moves no payload bytes but is still signalled, so a correct receiver's
+// check must fail; read on every call
+int skip_push_knob() {
+    const char* v = getenv("MPX_TEST_SKIP_PUSH");
+    return v ? atoi(v) : 0;
 }
 
 // A rank's stream must own its hardware queue.  The two halves of a pair
@@ -363,6 +409,13 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.nb_publish = nb_publish();
     a.ll_max = ll_max_bytes(same_device(me, peer));
     if (const char* v = getenv("MPX_LL_MAX")) a.ll_max = atoi(v) < kLLMaxBytes ? atoi(v) : kLLMaxBytes;
+    a.ring = me.ring;
+    a.peer_ring = peer.ring;
+    a.cnt = me.cnt;
+    a.slots = link_slots(me, peer, len);
+    a.skip_push = skip_push_knob();
+    if (a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!me.ring || !peer.ring))
+        return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
 
     const bool ll = mode != MPX_MODE_NONBLOCKING && len <= a.ll_max;
     const bool pushes_len = mode != MPX_MODE_UNIDIR || group == 1;
@@ -386,10 +439,15 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
         if (chunk <= kStageMaxBytes && chunk <= lds_cap) a.stage = (int)chunk;
     }
 
-    HIPCK(hipMemsetAsync(me.scratch, 0, 2 * sizeof(u64), me.stream));
-    if (a.check) HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
+    HIPCK(hipMemsetAsync(me.scratch, 0, 4 * sizeof(u64), me.stream));
+    if (a.check) {
+        HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
+        if (mode == MPX_MODE_NONBLOCKING) HIPCK(hipMemsetAsync(me.cnt, 0, (size_t)iters * sizeof(u64), me.stream));
+    }
     me.status->err = 0;
     me.status->where = 0;
+    me.status->recv_done = 0;
+    me.status->recv_digest = 0;
 
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
@@ -403,6 +461,8 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     t->launches = 1;
     t->nwg = ll ? 1 : a.nwg;
     t->protocol = ll ? kProtoLL : kProtoBulk;
+    t->recv_done = __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE);
+    t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
     const unsigned err = __atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE);
     if (err) {
         me.broken = true;
@@ -420,12 +480,21 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
 // ---------------------------------------------------------------------------
 // check mode for the stream engines: checksum the received bytes into
 // csum[i], then poison them — stream-ordered before the next push.
-int stream_check(Rank& me, long long n, int i, int iters) {
+int stream_check(Rank& me, long long n, int i, int iters, unsigned char* buf = nullptr) {
     if (n <= 0) return MPX_OK;
-    HIPCK(launch_checksum(me.rx, (size_t)n, me.csum + i, me.stream));
+    if (!buf) buf = me.rx;
+    HIPCK(launch_checksum(buf, (size_t)n, me.csum + i, me.stream));
     if (i + 1 < iters)   // the last payload stays in rx, as in the reference
-        HIPCK(launch_fill(me.rx, (size_t)n, MPX_FILL_BYTE, (0x5a ^ i) & 0xff, me.stream));
+        HIPCK(launch_fill(buf, (size_t)n, MPX_FILL_BYTE, (0x5a ^ i) & 0xff, me.stream));
     return MPX_OK;
+}
+
+// non-blocking publish schedule shared by the kernel and SDMA engines: every
+// nb_publish() pushes, at window slot 254 (the last receive a Waitall(255)
+// waits for, so no flush waits for the slot-255 push the reference leaves
+// pending) and at the last push
+bool nb_publishes(int i, int iters) {
+    return (i + 1) % nb_publish() == 0 || i % kNbWindow == kNbWindow - 2 || i + 1 == iters;
 }
 
 struct SdmaOps {
@@ -436,13 +505,14 @@ struct SdmaOps {
     const u64* txb = nullptr;   // graph capture: seqs relative to these device words
     const u64* rxb = nullptr;
     int launches = 0;
+    int skip = 0;               // test knob: 1 + iteration whose copy is skipped
     // The flag store is a one-lane kernel ordered after the copy on this
     // stream (hipStreamWriteValue64 measured slower, 10.9 vs 8.6 us per
     // iteration, profiles/r01_sdma_signal_ab.jsonl).  Waits are bounded
     // one-lane kernels: a stream-level wait (hipStreamWaitValue64) cannot
     // time out.
-    int push(long long n, u64 seq, bool publish = true) {
-        if (n > 0) {
+    int push(long long n, u64 seq, bool publish = true, bool skip_copy = false) {
+        if (n > 0 && !skip_copy) {
             HIPCK(hipMemcpyAsync(peer.rx, me.tx, (size_t)n, hipMemcpyDeviceToDevice, me.stream));
             ++launches;
         }
@@ -461,28 +531,29 @@ struct SdmaOps {
     // payload where the reference's Recv returns (before the reply / ack);
     // *inflight is the non-blocking window fill
     int step(int mode, int group, long long len, int i, int iters, u64 tx0, u64 rx0, bool check, int* inflight) {
+        const bool sk = skip == i + 1;
         if (mode == MPX_MODE_PINGPONG) {
             if (group == 1) {
-                TRY(push(len, tx0 + i + 1));
+                TRY(push(len, tx0 + i + 1, true, sk));
                 TRY(wait(rx0 + i + 1));
                 if (check) TRY(stream_check(me, len, i, iters));
             } else {
                 TRY(wait(rx0 + i + 1));
                 if (check) TRY(stream_check(me, len, i, iters));
-                TRY(push(len, tx0 + i + 1));
+                TRY(push(len, tx0 + i + 1, true, sk));
             }
         } else if (mode == MPX_MODE_UNIDIR) {
             if (group == 1) {
-                TRY(push(len, tx0 + i + 1));
+                TRY(push(len, tx0 + i + 1, true, sk));
                 TRY(wait(rx0 + i + 1));
                 if (check) TRY(stream_check(me, 1, i, iters));
             } else {
                 TRY(wait(rx0 + i + 1));
                 if (check) TRY(stream_check(me, len, i, iters));
-                TRY(push(1, tx0 + i + 1));                  // Send(tx, 1): always one byte
+                TRY(push(1, tx0 + i + 1, true, sk));        // Send(tx, 1): always one byte
             }
         } else {
-            TRY(push(len, tx0 + i + 1, (i + 1) % nb_publish() == 0 || i + 1 == iters));
+            TRY(push(len, tx0 + i + 1, nb_publishes(i, iters), sk));
             if (*inflight == kNbWindow - 1) {
                 TRY(wait(rx0 + i));                          // Waitall(255): not slot 255's receive
                 *inflight = 0;
@@ -490,6 +561,50 @@ struct SdmaOps {
                 ++*inflight;
             }
         }
+        return MPX_OK;
+    }
+
+    // The non-blocking loop in check mode, stream-ordered (the kernel
+    // engine's k_xfer_nbcheck in host-enqueued form): receive i lands in slot
+    // ring_slot(i) of the receiver; before a push reuses a slot the sender's
+    // stream waits for the receiver's credit; each receive is waited for,
+    // checksummed and poisoned right after this side's push i (so the two
+    // streams never wait on each other in a cycle), and the device counts
+    // the reference's Waitall receives (k_account at each flush).
+    int nb_checked(int iters, long long len, u64 tx0, u64 rx0, int slots) {
+        u64* credit_out = &peer.mb->credit[my_slot][0];
+        const u64* credit_in = &me.mb->credit[peer_slot][0];
+        TRY(signal_abs(credit_out, rx0));            // this call starts
+        int inflight = 0;
+        for (int i = 0; i < iters; ++i) {
+            TRY(wait_abs(credit_in, tx0 + (u64)(i >= slots ? i - slots + 1 : 0)));
+            if (len > 0 && skip != i + 1) {
+                HIPCK(hipMemcpyAsync(slot_ptr(peer, i, iters, slots, len), me.tx, (size_t)len,
+                                     hipMemcpyDeviceToDevice, me.stream));
+                ++launches;
+            }
+            TRY(signal_abs(&peer.mb->flag[my_slot][0], tx0 + i + 1));
+            TRY(wait_abs(&me.mb->flag[peer_slot][0], rx0 + i + 1));
+            TRY(stream_check(me, len, i, iters, slot_ptr(me, i, iters, slots, len)));
+            TRY(signal_abs(credit_out, rx0 + i + 1));
+            if (inflight == kNbWindow - 1) {          // Waitall(255): iterations i-255 .. i-1
+                HIPCK(launch_account(me.status, me.csum, i - inflight, inflight, len, me.stream));
+                inflight = 0;
+            } else {
+                ++inflight;
+            }
+        }
+        if (inflight > 0) HIPCK(launch_account(me.status, me.csum, iters - inflight, inflight, len, me.stream));
+        return MPX_OK;
+    }
+    int signal_abs(u64* flag, u64 v) {
+        HIPCK(launch_signal(flag, nullptr, v, me.stream));
+        ++launches;
+        return MPX_OK;
+    }
+    int wait_abs(const u64* flag, u64 v) {
+        HIPCK(launch_wait(flag, nullptr, v, me.status, tmo, me.stream));
+        ++launches;
         return MPX_OK;
     }
 };
@@ -523,11 +638,11 @@ int sdma_chunk_graph(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode,
         *out = it->second;
         return MPX_OK;
     }
-    SdmaOps cap{me, peer, my_rank, peer_rank, tmo, me.scratch + 2, me.scratch + 3};
+    SdmaOps cap{me, peer, my_rank, peer_rank, tmo, me.scratch + kScrSeqBase, me.scratch + kScrSeqBase + 1};
     HIPCK(hipStreamBeginCapture(me.stream, hipStreamCaptureModeThreadLocal));
     int inflight = 0, st = MPX_OK;
     for (int j = 0; j < count && st == MPX_OK; ++j) st = cap.step(mode, group, len, j, count, 0, 0, false, &inflight);
-    if (st == MPX_OK) st = launch_seqbase(me.scratch + 2, count, count, 1, me.stream) == hipSuccess
+    if (st == MPX_OK) st = launch_seqbase(me.scratch + kScrSeqBase, count, count, 1, me.stream) == hipSuccess
                                ? MPX_OK : fail(MPX_ERR_HIP, "k_seqbase launch in capture");
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(me.stream, &g);
@@ -549,10 +664,16 @@ int sdma_chunk_graph(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode,
 int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters, long long len,
              const mpx_xfer_opts* o, mpx_timing* t) {
     SdmaOps op{me, peer, my_rank, peer_rank, timeout_ticks(o)};
+    op.skip = skip_push_knob();
     const int check = (o && o->check) ? 1 : 0;
+    const int slots = link_slots(me, peer, len);
+    if (check && mode == MPX_MODE_NONBLOCKING && len > 0 && slots > 1 && (!me.ring || !peer.ring))
+        return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
     if (check) HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
     me.status->err = 0;
     me.status->where = 0;
+    me.status->recv_done = 0;
+    me.status->recv_digest = 0;
     const u64 txs0 = me.tx_seq[peer_rank], rxs0 = me.rx_seq[peer_rank];
     // graph-replayed chunks for the bulk of the loop (not in check mode,
     // whose per-iteration checksum slots would move with every chunk)
@@ -562,15 +683,24 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     hipGraphExec_t full = nullptr, tail = nullptr;
     if (chunks > 0) TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, kSdmaChunk, &full));
     if (rest > 0) TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, rest, &tail));
-    if (full || tail) HIPCK(launch_seqbase(me.scratch + 2, txs0, rxs0, 0, me.stream));
+    if (full || tail) HIPCK(launch_seqbase(me.scratch + kScrSeqBase, txs0, rxs0, 0, me.stream));
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
-    for (int c = 0; c < chunks; ++c) HIPCK(hipGraphLaunch(full, me.stream));
-    if (tail) HIPCK(hipGraphLaunch(tail, me.stream));
-    int inflight = 0;
-    const int replayed = chunks * kSdmaChunk + rest;
-    for (int i = replayed; i < iters; ++i) TRY(op.step(mode, group, len, i, iters, txs0, rxs0, check, &inflight));
-    if (mode == MPX_MODE_NONBLOCKING && iters > 0 && (iters % kNbWindow) != 0) TRY(op.wait(rxs0 + iters));
+    if (check && mode == MPX_MODE_NONBLOCKING) {
+        TRY(op.nb_checked(iters, len, txs0, rxs0, slots));
+    } else {
+        for (int c = 0; c < chunks; ++c) HIPCK(hipGraphLaunch(full, me.stream));
+        if (tail) HIPCK(hipGraphLaunch(tail, me.stream));
+        int inflight = 0;
+        const int replayed = chunks * kSdmaChunk + rest;
+        for (int i = replayed; i < iters; ++i) TRY(op.step(mode, group, len, i, iters, txs0, rxs0, check, &inflight));
+        if (mode == MPX_MODE_NONBLOCKING && iters > 0 && (iters % kNbWindow) != 0) TRY(op.wait(rxs0 + iters));
+        // every receive of ping-pong / unidir is complete here; the device
+        // counts them and digests their checksums
+        if (check && iters > 0)
+            HIPCK(launch_account(me.status, me.csum, 0, iters,
+                                 (mode == MPX_MODE_UNIDIR && group == 1) ? 1 : len, me.stream));
+    }
     HIPCK(hipEventRecord(me.ev1, me.stream));
     HIPCK(hipEventSynchronize(me.ev1));
     t->wall_s = now_s() - t0;
@@ -580,6 +710,11 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     t->launches = op.launches + (chunks + (tail ? 1 : 0));   // graph replays count once each
     t->nwg = 0;
     t->protocol = kProtoSdma;
+    // check mode: counted on the device (k_account); otherwise the loop's
+    // structure fixes the count
+    t->recv_done = check ? __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE)
+                         : (mode == MPX_MODE_NONBLOCKING ? nb_waited(iters) : (u64)iters);
+    t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
     if (__atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE)) {
         me.broken = true;
         return fail(MPX_ERR_TIMEOUT, "rank %d <- rank %d: SDMA-engine wait timed out", my_rank, peer_rank);
@@ -599,42 +734,65 @@ int run_rccl(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     if (!me.comm) return fail(MPX_ERR_STATE, "rank %d has no RCCL communicator (mpx_rccl_init_*)", my_rank);
     const int check = (o && o->check) ? 1 : 0;
     if (check) HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
+    me.status->recv_done = 0;
+    me.status->recv_digest = 0;
     const size_t n = (size_t)len;
+    const int skip = skip_push_knob();
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
-    int launches = 0;
+    int launches = 0, inflight = 0;
     for (int i = 0; i < iters; ++i) {
+        // test knob: the "lost" send carries rx (poison or stale bytes), not tx
+        const void* src = skip == i + 1 ? (const void*)me.rx : (const void*)me.tx;
         if (mode == MPX_MODE_PINGPONG) {
             if (group == 1) {
-                NCCLCK(ncclSend(me.tx, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
                 NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, len, i, iters));
             } else {
                 NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, len, i, iters));
-                NCCLCK(ncclSend(me.tx, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
             }
             launches += 2;
         } else if (mode == MPX_MODE_UNIDIR) {
             if (group == 1) {
-                NCCLCK(ncclSend(me.tx, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
                 NCCLCK(ncclRecv(me.rx, 1, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, 1, i, iters));
             } else {
                 NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, len, i, iters));
-                NCCLCK(ncclSend(me.tx, 1, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(ncclSend(src, 1, ncclChar, peer_rank, me.comm, me.stream));
             }
             launches += 2;
         } else {
-            // Isend + Irecv of one iteration: one fused group (full duplex)
+            // Isend + Irecv of one iteration: one fused group (full duplex).
+            // Check mode: the receive lands in rx and is checksummed (and
+            // poisoned) on this stream before the next group's receive can
+            // land — RCCL writes only this rank's own buffer, so no slots or
+            // credits are needed; the device counts the Waitall receives.
             NCCLCK(ncclGroupStart());
-            NCCLCK(ncclSend(me.tx, n, ncclChar, peer_rank, me.comm, me.stream));
+            NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
             NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
             NCCLCK(ncclGroupEnd());
             launches += 1;
+            if (check) {
+                TRY(stream_check(me, len, i, iters));
+                if (inflight == kNbWindow - 1) {       // Waitall(255): iterations i-255 .. i-1
+                    HIPCK(launch_account(me.status, me.csum, i - inflight, inflight, len, me.stream));
+                    inflight = 0;
+                } else {
+                    ++inflight;
+                }
+            }
         }
     }
+    if (check && mode == MPX_MODE_NONBLOCKING && inflight > 0)
+        HIPCK(launch_account(me.status, me.csum, iters - inflight, inflight, len, me.stream));
+    if (check && mode != MPX_MODE_NONBLOCKING && iters > 0)
+        HIPCK(launch_account(me.status, me.csum, 0, iters, (mode == MPX_MODE_UNIDIR && group == 1) ? 1 : len,
+                             me.stream));
     HIPCK(hipEventRecord(me.ev1, me.stream));
     HIPCK(hipEventSynchronize(me.ev1));
     t->wall_s = now_s() - t0;
@@ -644,6 +802,9 @@ int run_rccl(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     t->launches = launches;
     t->nwg = 0;
     t->protocol = kProtoRccl;
+    t->recv_done = check ? __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE)
+                         : (mode == MPX_MODE_NONBLOCKING ? nb_waited(iters) : (u64)iters);
+    t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
     return MPX_OK;
 }
 
@@ -739,6 +900,7 @@ int mpx_finalize(mpx_ctx* ctx) {
         if (!rk.local) continue;
         DeviceGuard g(rk.dev);
         if (rk.mb) (void)hipFree(rk.mb);
+        if (rk.ring) (void)hipFree(rk.ring);
         if (rk.scratch) (void)hipFree(rk.scratch);
         if (rk.csum) (void)hipFree(rk.csum);
         for (void* q : rk.retired) (void)hipFree(q);
@@ -917,8 +1079,19 @@ int mpx_rank_attach(mpx_ctx* ctx, int rank, int dev, void* tx, void* rx, size_t 
     HIPCK(hipEventCreate(&rk.ev1));
     HIPCK(hipHostMalloc(reinterpret_cast<void**>(&rk.status), sizeof(Status), hipHostMallocCoherent | hipHostMallocMapped));
     memset(rk.status, 0, sizeof(Status));
-    HIPCK(hipMalloc(&rk.scratch, 4 * sizeof(u64)));
+    HIPCK(hipMalloc(&rk.scratch, kScratchWords * sizeof(u64)));
+    HIPCK(hipMemsetAsync(rk.scratch, 0, kScratchWords * sizeof(u64), rk.stream));
     TRY(ensure_csum(rk, 1024));
+    // receive slots of non-blocking check mode (IPC-exportable like rx)
+    rk.ring_bytes = ring_bytes_for(len);
+    if (rk.ring_bytes) {
+        void* p = nullptr;
+        const hipError_t e = hipMalloc(&p, rk.ring_bytes);
+        if (e == hipErrorOutOfMemory) return fail(MPX_ERR_NOMEM, "check ring of %llu B on device %d",
+                                                  (unsigned long long)rk.ring_bytes, dev);
+        HIPCK(e);
+        rk.ring = static_cast<unsigned char*>(p);
+    }
     HIPCK(hipStreamSynchronize(rk.stream));
 
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -961,6 +1134,8 @@ int mpx_rank_export(mpx_ctx* ctx, int rank, void* desc) {
     DBG("export rank %d: rx %p mb %p (kind %d) dev %d\n", rank, (void*)rk.rx, (void*)rk.mb, rk.mb_kind, rk.dev);
     HIPCK(hipIpcGetMemHandle(&d.rx_handle, rk.rx));
     HIPCK(hipIpcGetMemHandle(&d.mb_handle, rk.mb));
+    d.ring_bytes = rk.ring_bytes;
+    if (rk.ring) HIPCK(hipIpcGetMemHandle(&d.ring_handle, rk.ring));
     memset(desc, 0, MPX_RANK_DESC_BYTES);
     memcpy(desc, &d, sizeof d);
     return MPX_OK;
@@ -992,6 +1167,12 @@ int mpx_rank_import(mpx_ctx* ctx, int rank, const void* desc) {
     HIPCK(hipIpcOpenMemHandle(&p, d.rx_handle, hipIpcMemLazyEnablePeerAccess));
     ctx->ipc_opened.push_back(p);
     rk.rx = static_cast<unsigned char*>(p);
+    rk.ring_bytes = d.ring_bytes;
+    if (d.ring_bytes) {
+        HIPCK(hipIpcOpenMemHandle(&p, d.ring_handle, hipIpcMemLazyEnablePeerAccess));
+        ctx->ipc_opened.push_back(p);
+        rk.ring = static_cast<unsigned char*>(p);
+    }
     ctx->r[rank] = rk;
     return MPX_OK;
 }
@@ -1031,7 +1212,9 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     }
     if (st != MPX_OK) return st;
     t->bytes = (uint64_t)buff_len * (uint64_t)iters * (mode == MPX_MODE_UNIDIR ? 1u : 2u);
-    if (check && mode != MPX_MODE_NONBLOCKING && iters > 0) {
+    // every received payload — in the non-blocking loop too, where each
+    // receive has a slot of its own (k_xfer_nbcheck / SdmaOps::nb_checked)
+    if (check && iters > 0) {
         std::vector<u64> raw((size_t)iters);
         // the rank's own stream: a null-stream copy would wait for every
         // blocking stream of the device, i.e. for other pairs' kernels

@@ -191,7 +191,8 @@ static void open_logs(int rank, rank_files *f)
     f->gpu_fp = fopen(name, "w");
     if (f->gpu_fp)
         fprintf(f->gpu_fp, "Timestamp,JobId,Rank,Engine,Mode,Device,PeerRank,PeerDevice,BufferSize,NumOfBuffers,"
-                           "WallTimems,DeviceTimems,GBps,Protocol,Workgroups,CheckedPayloads,CheckFailures,RunId\n");
+                           "WallTimems,DeviceTimems,GBps,Protocol,Workgroups,CheckedPayloads,CheckFailures,RunId,RecvDone,"
+                           "RecvDigest\n");
     f->t_last_logtime = wtime();
 }
 
@@ -272,11 +273,12 @@ static void *rank_main(void *arg)
                 if (files.gpu_fp) {
                     const double gbps = my_time > 0 ? (double)tm.bytes / my_time / 1e9 : 0.0;
                     static const char *proto[] = {"ll", "bulk", "sdma", "rccl", "copy"};
-                    fprintf(files.gpu_fp, "%s,%s,%d,%s,%d,%d,%d,%d,%d,%d,%.4f,%.4f,%.3f,%s,%d,%llu,%d,%lld\n", ts,
+                    fprintf(files.gpu_fp, "%s,%s,%d,%s,%d,%d,%d,%d,%d,%d,%.4f,%.4f,%.3f,%s,%d,%llu,%d,%lld,%llu,%llu\n", ts,
                             opt.uuid, r, mpxh_engine_name(opt.engine), xfer_mode(), dev_of[r], peer, dev_of[peer], B,
                             opt.iters, my_time * 1e3, tm.device_s * 1e3, gbps,
                             (tm.protocol >= 0 && tm.protocol <= 4) ? proto[tm.protocol] : "?", tm.nwg,
-                            (unsigned long long)tm.check_iters, tm.check_failures, run_idx);
+                            (unsigned long long)tm.check_iters, tm.check_failures, run_idx,
+                            (unsigned long long)tm.recv_done, (unsigned long long)tm.recv_digest);
                 }
             }
 
@@ -487,9 +489,10 @@ int main(int argc, char **argv)
             }
             dev = gl[local_rank];
         }
-        char ip[MPXH_MAX_HOST];
-        snprintf(ip, sizeof ip, "%s:gpu%d", node_ip, dev);
-        share_node_info(node, ip, dev);
+        /* LocalIP / RemoteIP of the records and INFO lines: the IPv4 of the
+           rank's host, as get_ipaddress(processor name) gives it in the
+           reference (mpi_perf.c:236-237,553); the GPU ids go to gpu-*.csv */
+        share_node_info(node, node_ip, dev);
     } else {
         for (int r = 0; r < world; ++r) snprintf(host_of[r], MPXH_MAX_HOST, "%s", node);
     }
@@ -567,7 +570,7 @@ int main(int argc, char **argv)
                 fprintf(stderr, "rank %d: GPU %d not visible (%d GPUs)\n", r, dev_of[r], ndev);
                 mpx_abort();
             }
-            snprintf(ip_of[r], sizeof ip_of[r], "%s:gpu%d", node_ip, dev_of[r]);
+            snprintf(ip_of[r], sizeof ip_of[r], "%s", node_ip); /* the host's IPv4, mpi_perf.c:236-237 */
         }
     }
     if (!opt.all_pairs && !win_cli) {

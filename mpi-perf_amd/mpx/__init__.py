@@ -28,6 +28,7 @@ MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
 MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": MODE_UNIDIR}
 FILL_BYTE, FILL_SPLITMIX = 0, 1
 XFER_STREAM = 1
+ABI_VERSION = 2
 PATTERN_SEED = 0x6D70695F70657266
 MAX_RANKS = 16
 RANK_DESC_BYTES = 512
@@ -45,6 +46,8 @@ class Timing(C.Structure):
         ("protocol", C.c_int32),
         ("check_failures", C.c_int32),
         ("check_iters", C.c_uint64),
+        ("recv_done", C.c_uint64),
+        ("recv_digest", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -110,6 +113,9 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.mpx_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: ABI version {L.mpx_version()}, this binding needs {ABI_VERSION} "
+                              "(stale build: run __graft_entry__.build())")
         _lib = L
     return _lib
 

@@ -46,7 +46,8 @@ def main():
             t = c.xfer(mode, group, rank, peer, iters, tx, rx, n, check_payload=True,
                        expect=peer_sums[str(n)], expect_ack=peer_sums["1"], timeout_ms=5000)
             m = 1 if (mode == mpx.MODE_UNIDIR and group == 1) else n
-            results.append(dict(mode=mode, n=n, check_iters=t.check_iters, check_failures=t.check_failures,
+            results.append(dict(mode=mode, n=n, iters=iters, check_iters=t.check_iters,
+                                check_failures=t.check_failures, recv_done=t.recv_done,
                                 final_rx_ok=c.checksum(rx, m) == peer_sums[str(m)], protocol=t.protocol,
                                 us_per_iter=t.wall_s / iters * 1e6))
     with open(os.path.join(d, f"result_{rank}.json"), "w") as f:

@@ -21,7 +21,7 @@ for engine in ("kernel", "sdma"):
             bufs.append((tx, rx))
         for mode in (mpx.MODE_PINGPONG, mpx.MODE_NONBLOCKING, mpx.MODE_UNIDIR):
             for n, iters, check in [(8, 300, False), (4100, 7, True), (70001, 5, True), (CAP, 3, True),
-                                    (65541, 519, False)]:
+                                    (65541, 519, False), (4100, 300, True)]:
                 exp = {r: (c.checksum(bufs[1 - r][0], n), c.checksum(bufs[1 - r][0], 1)) for r in (0, 1)}
                 errs = []
 

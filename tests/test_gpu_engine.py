@@ -130,8 +130,8 @@ def test_loopback_pair_every_payload(engine, mode):
             assert not errs, (n, errs)
             for r in (0, 1):
                 t = out[r]
-                if mode != mpx.MODE_NONBLOCKING:
-                    assert t.check_iters == iters and t.check_failures == 0, (n, r)
+                assert t.check_iters == iters and t.check_failures == 0, (n, r)
+                assert t.recv_done == (O.lib().oracle_nb_waited(iters) if mode == mpx.MODE_NONBLOCKING else iters)
                 assert t.bytes == n * iters * (1 if mode == mpx.MODE_UNIDIR else 2)
             # the delivered bytes: G0 rx = G1's tx; G1 rx = G0's tx (all of it,
             # or its first byte for unidir's 1-byte ack, mpi_perf.c:137,142)
@@ -165,8 +165,7 @@ def test_push_widths_staged_and_unstaged(mode, stream):
                 pushes = mode != mpx.MODE_UNIDIR or r == 0
                 if pushes:
                     assert out[r].nwg == nwg and out[r].protocol == 1, (nwg, n, r)
-                if mode != mpx.MODE_NONBLOCKING:
-                    assert out[r].check_failures == 0 and out[r].check_iters == 5
+                assert out[r].check_failures == 0 and out[r].check_iters == 5
                 m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else n
                 assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (nwg, n, r)
     finally:
@@ -190,8 +189,7 @@ def test_sdma_graph_chunks_keep_sequence_state(mode):
                 assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (n, r)
             out, errs = P.run(mode, n, 5, check=True)
             assert not errs, (n, "checked run after chunks", errs)
-            if mode != mpx.MODE_NONBLOCKING:
-                assert all(out[r].check_failures == 0 and out[r].check_iters == 5 for r in (0, 1))
+            assert all(out[r].check_failures == 0 and out[r].check_iters == 5 for r in (0, 1))
     finally:
         P.close()
 
@@ -217,7 +215,11 @@ def _digest_cases():
 def test_receive_digest_matches_reference(name, engine):
     """Runs the golden case's configuration (pairs, mode, B, iters, runs) on the
     GPU with every payload checksummed, and compares each rank's receive
-    digest with what the compiled reference's ranks received."""
+    accounting — counted on the device: which receives completed (every
+    Recv; the requests each Waitall of the non-blocking loop waited for),
+    their bytes, and the sum of their checksums — with what the compiled
+    reference's ranks received (the PMPI shim's recv_done / recv_bytes /
+    recv_digest).  Nothing here comes from the oracle."""
     c = GOLDEN[name]
     a = c["args"]
     ppn = c["ppn"]
@@ -234,19 +236,64 @@ def test_receive_digest_matches_reference(name, engine):
             for r in range(2 * ppn):
                 ack = mode == mpx.MODE_UNIDIR and P.group(r) == 1
                 m = 1 if ack else B
-                if mode == mpx.MODE_NONBLOCKING:
-                    k = O.lib().oracle_nb_waited(iters)
-                    one = P.c.checksum(P.bufs[r][1], m)   # every receive carries the same bytes
-                else:
-                    assert out[r].check_failures == 0 and out[r].check_iters == iters
-                    k = iters
-                    one = P.expect(r, m)[0]
-                digest[r][0] += k
-                digest[r][1] += k * m
-                digest[r][2] = (digest[r][2] + k * one) & 0xFFFFFFFFFFFFFFFF
+                assert out[r].check_failures == 0 and out[r].check_iters == iters
+                digest[r][0] += out[r].recv_done
+                digest[r][1] += out[r].recv_done * m
+                digest[r][2] = (digest[r][2] + out[r].recv_digest) & 0xFFFFFFFFFFFFFFFF
         for r in range(2 * ppn):
             ref = c["shim"][str(r)]
             assert digest[r] == [ref["recv_done"], ref["recv_bytes"], ref["recv_digest"]], r
+    finally:
+        P.close()
+
+
+NB_ITERS = [1, 254, 255, 256, 257, 511, 512, 600]
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+@pytest.mark.parametrize("n", [0, 1, 4097, 65541, 456131])
+def test_nonblocking_every_payload_seeded(engine, n):
+    """-x 1 with seeded payloads: every one of the (up to 256 concurrent)
+    receives is checksummed on the device in a slot of its own; the device
+    counts exactly the receives the reference's Waitall calls complete
+    (iters - iters // 256: slot 255 of each full window is never waited
+    for, mpi_perf.c:108-111) and digests them; rx ends holding the last
+    payload."""
+    P = Pairs(engine, 1, max(n, 1), fill="seeded")
+    try:
+        for iters in NB_ITERS:
+            out, errs = P.run(mpx.MODE_NONBLOCKING, n, iters)
+            assert not errs, (iters, errs)
+            for r in (0, 1):
+                t = out[r]
+                assert t.check_iters == iters and t.check_failures == 0, (iters, r)
+                k = iters - iters // 256
+                assert k == O.lib().oracle_nb_waited(iters)
+                assert t.recv_done == k, (iters, r, t.recv_done)
+                one = P.expect(r, n)[0]
+                assert t.recv_digest == (k * one) & 0xFFFFFFFFFFFFFFFF, (iters, r)
+                assert P.c.checksum(P.bufs[r][1], n) == one
+    finally:
+        P.close()
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("skip", [1, 7, 256])
+def test_lost_payload_fails_the_check(monkeypatch, engine, mode, skip):
+    """Test knob MPX_TEST_SKIP_PUSH=k: the k-th push of each call moves no
+    payload bytes but is still signalled.  Check mode must then report the
+    receive that never got its payload (a checker that only looked at the
+    final rx, or took receive counts from elsewhere, would pass)."""
+    monkeypatch.setenv("MPX_TEST_SKIP_PUSH", str(skip))
+    n = 65541 if skip != 7 else 1000   # 1000 B: the LL protocol for ping-pong / unidir
+    P = Pairs(engine, 1, n, fill="seeded")
+    try:
+        out, errs = P.run(mode, n, 300)
+        for r in (0, 1):
+            receives_payload = not (mode == mpx.MODE_UNIDIR and r == 0)   # G1 receives 1-byte acks
+            if receives_payload:
+                assert r in errs and errs[r].status == mpx.ERR_CHECK, (r, errs, out.get(r))
     finally:
         P.close()
 
@@ -345,7 +392,7 @@ PROTO_LL = 0
 @pytest.mark.parametrize("knobs", [
     {"MPX_STAGE": "0", "MPX_NB_PUBLISH": "1", "MPX_SDMA_GRAPH": "0"},
     {"MPX_PUSH_STREAM": "1", "MPX_LL_FLAGS": "4", "MPX_NB_PUBLISH": "256", "MPX_PUSH_WG": "7"},
-    {"MPX_LL_MAX": "8192", "MPX_NB_PUBLISH": "2"},
+    {"MPX_LL_MAX": "8192", "MPX_NB_PUBLISH": "2", "MPX_CHECK_RING_BYTES": "0"},   # one receive slot per link
 ])
 def test_env_knob_variants(knobs):
     """The documented MPX_* knobs switch code paths that the
@@ -389,8 +436,7 @@ def test_max_size_pairs_every_mode(engine):
                 out, errs = P.run(mode, INT_MAX, 2, timeout_ms=30000, nwg=nwg)
                 assert not errs, (mode, nwg, errs)
                 for r in (0, 1):
-                    if mode != mpx.MODE_NONBLOCKING:
-                        assert out[r].check_iters == 2 and out[r].check_failures == 0, (mode, nwg, r)
+                    assert out[r].check_iters == 2 and out[r].check_failures == 0, (mode, nwg, r)
                     m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else INT_MAX
                     assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (mode, nwg, r)
     finally:

@@ -21,7 +21,9 @@ def run(tmp_path, args, lines=("vm",), names="vm,runsc", gpus="0,0"):
     g1.write_text("".join(x + "\n" for x in lines))
     logs = tmp_path / "logs"
     argv = [a.replace("@G1", str(g1)).replace("@LOGS", str(logs)) for a in args]
-    env = dict(os.environ, MPX_PROCESSOR_NAMES=names)
+    # MPX_HOSTNAME=localhost: the ranks' host IPv4 is 127.0.0.1, as in the
+    # golden runs, so whole record lines compare (mpi_perf.c:236-237,551-554)
+    env = dict(os.environ, MPX_PROCESSOR_NAMES=names, MPX_HOSTNAME="localhost")
     p = subprocess.run([PERF, "-g", gpus, "-t", "5000"] + argv, capture_output=True, text=True, env=env, timeout=120)
     recs = []
     for f in sorted(glob.glob(str(logs / "tcp-*.log"))):
@@ -48,10 +50,9 @@ def test_records_match_reference_run(tmp_path, name):
                         names=names, gpus=gpus)
     assert p.returncode == 0, p.stderr[-600:]
     assert len(recs) == c["n_records"]
-    ref = sorted((r["rank"], r["vmcount"], r["flows"], r["buffer_size"], r["num_buffers"], r["run_id"])
-                 for r in c["records"])
-    mine = sorted((int(f[2]), int(f[3]), int(f[6]), int(f[7]), int(f[8]), int(f[10])) for f in recs)
-    assert mine[:len(ref)] == ref
+    # whole record lines (timestamp, job id and time masked), LocalIP /
+    # RemoteIP included; the golden keeps a sample of long runs' records
+    assert_records_match(recs, c)
     for f in recs:
         assert len(f) == 11 and re.fullmatch(r"\d{4}-\d\d-\d\d \d\d:\d\d:\d\d", f[0])
         assert re.fullmatch(r"\d+\.\d\d", f[9])
@@ -60,10 +61,29 @@ def test_records_match_reference_run(tmp_path, name):
                       r"group_rank: (\d+), my_peer: (-?\d+)", p.stderr)
     assert sorted((int(x[1]), int(x[3]), int(x[4]), int(x[5]), int(x[6])) for x in info) == \
         sorted((d["rank"], d["group"], d["group_size"], d["group_rank"], d["peer"]) for d in c["info"])
-    # every checked payload passed
+    # every payload checked and passed, in every mode; each run's receives,
+    # counted on the device, are the reference's (shim totals over all runs)
+    runs = int(c["args"][c["args"].index("-r") + 1])
     for f in side:
-        if f[4] != "1":       # nonblocking: final rx only
-            assert int(f[16]) == 0 and int(f[15]) == int(f[9])
+        assert int(f[16]) == 0 and int(f[15]) == int(f[9])
+        ref = c["shim"][f[2]]
+        assert int(f[18]) * runs == ref["recv_done"]
+        assert (int(f[19]) * runs) & 0xFFFFFFFFFFFFFFFF == ref["recv_digest"]
+
+
+def assert_records_match(recs, c):
+    from collections import Counter
+    mine = Counter(mask_record(f) for f in recs)
+    ref = Counter(r["line_masked"] for r in c["records"])
+    assert not ref - mine, (ref - mine, sorted(mine)[:8])
+    if len(c["records"]) == c["n_records"]:
+        assert mine == ref
+
+
+def mask_record(f):
+    """a tcp-*.log record with the fields the golden masks (mpi_perf.c:551):
+    timestamp T, job id U, time X"""
+    return ",".join(["T", "U"] + f[2:9] + ["X", f[10]])
 
 
 def test_seeded_pattern_check_and_sweep(tmp_path):
@@ -121,7 +141,8 @@ def test_log_rotation_and_ingest_hook(tmp_path):
     env_cmd = f"echo ingest >> {hook}"
     g1 = tmp_path / "group1"
     g1.write_text("vm\n")
-    env = dict(os.environ, MPX_PROCESSOR_NAMES="vm,runsc", MPX_LOG_REFRESH_SEC="0.001", MPX_INGEST_CMD=env_cmd)
+    env = dict(os.environ, MPX_PROCESSOR_NAMES="vm,runsc", MPX_LOG_REFRESH_SEC="0.001", MPX_INGEST_CMD=env_cmd,
+               MPX_HOSTNAME="localhost")
     p = subprocess.run([PERF, "-g", "0,0", "-w", "2", "-f", str(g1), "-n", "1", "-p", "1", "-u", "1", "-r", "6",
                         "-i", "20000", "-b", "8", "-l", str(tmp_path / "logs")], capture_output=True, text=True,
                        env=env, timeout=120)
@@ -133,6 +154,20 @@ def test_log_rotation_and_ingest_hook(tmp_path):
     assert opened >= 2 and len(files) >= 1
     total = sum(len(f.read_text().splitlines()) for f in files)
     assert 1 <= total <= 5
+    # what kusto_ingest.py would upload from this directory (kusto_ingest.py:
+    # 32-40, n = 1): every selected file parses as PerfLogsMPI rows
+    # (mpi_perf.c:550-554) of this job; the gpu-*.csv side files are never
+    # selected
+    import kusto_rule as K
+    picked = K.select(str(tmp_path / "logs"), 1)
+    assert len(picked) == len(files) - 1
+    assert not any(os.path.basename(f).startswith("gpu-") for f in picked)
+    for f in picked:
+        for line in open(f):
+            row = K.parse_row(line)
+            assert row["Rank"] == 0 and row["VMCount"] == 2 and row["NumOfFlows"] == 1
+            assert row["BufferSize"] == 8 and row["NumOfBuffers"] == 20000 and 1 <= row["RunId"] <= 5
+            assert row["LocalIP"] == row["RemoteIP"] == "127.0.0.1"
 
 
 # ---- processes mode: one mpx_perf process per rank (the reference's model) --
@@ -151,7 +186,7 @@ def run_procs(tmp_path, args, n, names, lines=("vm",)):
     ps = []
     for r in range(n):
         env = dict(os.environ, MPX_RANK=str(r), MPX_SIZE=str(n), MPX_LOCAL_RANK=str(r), MPX_PROCESSOR_NAMES=names,
-                   MPX_BOOTSTRAP=f"127.0.0.1:{port}", MPX_BOOTSTRAP_TIMEOUT="60")
+                   MPX_BOOTSTRAP=f"127.0.0.1:{port}", MPX_BOOTSTRAP_TIMEOUT="60", MPX_HOSTNAME="localhost")
         ps.append(subprocess.Popen([PERF, "-g", ",".join(["0"] * n), "-t", "5000"] + argv, stdout=subprocess.PIPE,
                                    stderr=subprocess.PIPE, text=True, env=env))
     errs = [p.communicate(timeout=120)[1] for p in ps]
@@ -180,10 +215,12 @@ def test_processes_mode_records_match_reference_run(tmp_path, engine, name):
                       r"group_rank: (\d+), my_peer: (-?\d+)", err)
     assert sorted((int(x[1]), int(x[3]), int(x[4]), int(x[5]), int(x[6])) for x in info) == \
         sorted((d["rank"], d["group"], d["group_size"], d["group_rank"], d["peer"]) for d in c["info"])
+    assert_records_match(recs, c)
+    runs = int(c["args"][c["args"].index("-r") + 1])
     for f in side:
         assert f[3] == engine
-        if f[4] != "1":
-            assert int(f[16]) == 0 and int(f[15]) == int(f[9])
+        assert int(f[16]) == 0 and int(f[15]) == int(f[9])
+        assert int(f[18]) * runs == c["shim"][f[2]]["recv_done"]
 
 
 def test_processes_mode_all_pairs_seeded_payloads(tmp_path):

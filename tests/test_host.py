@@ -147,7 +147,9 @@ def run_perf(args, tmp_path, lines=("vm",), names="vm,runsc"):
     g1 = tmp_path / "group1"
     g1.write_text("".join(x + "\n" for x in lines))
     argv = [a.replace("@G1", str(g1)).replace("@LOGS", str(tmp_path / "logs")) for a in args]
-    env = dict(os.environ, MPX_PROCESSOR_NAMES=names)
+    # MPX_HOSTNAME=localhost: this host's IPv4 is 127.0.0.1, as the golden
+    # runs resolved their ranks' processor names (mpi_perf.c:236-237)
+    env = dict(os.environ, MPX_PROCESSOR_NAMES=names, MPX_HOSTNAME="localhost")
     return subprocess.run([PERF] + argv, capture_output=True, text=True, env=env, timeout=60)
 
 
@@ -166,38 +168,44 @@ def test_cli_error_exits_match_reference(tmp_path, name):
     assert ("UUID: " in p.stderr) == c["uuid_printed"] or name in ("err_unknown_flag", "err_h_flag")
 
 
-def _mask_ip(line):
-    return re.sub(r"\d+\.\d+\.\d+\.\d+(:gpu\d+)?", "IP", line)
-
-
 def test_dotnet_mode_matches_reference(tmp_path):
     """-d 1 prints the launcher command per rank per run and writes no record
-    (mpi_perf.c:147-168, :545); it needs no GPU, like the reference."""
+    (mpi_perf.c:147-168, :545); it needs no GPU, like the reference.  The
+    lines are compared whole, IPv4 addresses included."""
     c = CASES["dotnet_print_only"]
     p = run_perf(["-w", "2"] + c["args"], tmp_path, lines=c["group1_lines"], names="vm,runsc")
     assert p.returncode == 0, p.stderr[-500:]
-    mine = sorted(_mask_ip(x) for x in re.findall(r"^dotnet .*$", p.stderr, flags=re.M))
-    assert mine == sorted(_mask_ip(x) for x in c["dotnet"])
+    mine = sorted(re.findall(r"^dotnet .*$", p.stderr, flags=re.M))
+    assert mine == sorted(c["dotnet"])
     logs = tmp_path / "logs"
     assert len(list(logs.glob("tcp-*.log"))) == len(c["files"]) == 1
     assert all(f.stat().st_size == 0 for f in logs.glob("tcp-*.log")) and c["n_records"] == 0
     assert ("[Run#: 0]" in p.stderr) == (c["summaries"] == [0])
 
 
-def test_kusto_file_selection_contract(tmp_path):
-    """kusto_ingest.py:32-40 ingests files in the log dir whose name starts with
-    'tcp' (case-insensitive), all but the newest n by mtime.  The GPU side
-    files must never be selected."""
+def test_kusto_file_selection_on_a_directory_mpx_perf_wrote(tmp_path):
+    """kusto_ingest.py:32-40's selection rule (tests/kusto_rule.py) applied to
+    the log directory an mpx_perf run really wrote: -d 1 (no GPU needed),
+    rotation every run (MPX_LOG_REFRESH_SEC), so several tcp-*.log files and
+    their gpu-*.csv side files.  Only tcp files are picked, oldest first,
+    all but the newest n; the side files never."""
     import time
+    import kusto_rule as K
+    g1 = tmp_path / "group1"
+    g1.write_text("vm\n")
     logs = tmp_path / "logs"
-    logs.mkdir()
-    names = ["tcp-u-0-2026-01-01-00-00-00.log", "tcp-u-0-2026-01-01-00-15-00.log", "gpu-u-0-x.csv",
-             "TCP-u-1-2026-01-01-00-00-00.log"]
-    for i, n in enumerate(names):
-        (logs / n).write_text("x\n")
-        os.utime(logs / n, (1000 + i, 1000 + i))
-    files = [f for f in os.listdir(logs) if (logs / f).is_file() and f.lower().startswith("tcp")]
-    files.sort(key=lambda f: os.path.getmtime(logs / f))
-    picked = files[:-1]
-    assert "gpu-u-0-x.csv" not in files and len(picked) == 2
-    del time
+    env = dict(os.environ, MPX_PROCESSOR_NAMES="vm,runsc", MPX_LOG_REFRESH_SEC="0")
+    for k in range(3):     # three jobs: log names differ by UUID (and second)
+        p = subprocess.run([PERF, "-w", "2", "-f", str(g1), "-n", "1", "-p", "1", "-d", "1", "-r", "2",
+                            "-l", str(logs)], capture_output=True, text=True, env=env, timeout=60)
+        assert p.returncode == 0, p.stderr[-400:]
+        time.sleep(0.02)
+    written = sorted(os.listdir(logs))
+    tcp = [f for f in written if f.startswith("tcp-")]
+    side = [f for f in written if f.startswith("gpu-")]
+    assert len(tcp) >= 3 and len(side) == len(tcp)
+    for n in (1, 2):
+        picked = K.select(str(logs), n)
+        assert [os.path.basename(f) for f in picked] == \
+            sorted(tcp, key=lambda f: os.path.getmtime(logs / f))[:-n]
+        assert not any(os.path.basename(f).startswith("gpu-") for f in picked)
