@@ -192,7 +192,12 @@ int mpx_rank_import(mpx_ctx *ctx, int rank, const void *desc);
    local rank `my_rank` (group `my_group`, 1 = sender side) and `peer_rank`,
    returning when this rank's side of the loop is complete, like the MPI loop.
    tx/rx must be the buffers attached for my_rank; buff_len <= attached len.
-   *sec (may be NULL) receives the wall time of the loop. */
+   *sec (may be NULL) receives the wall time of the loop.
+   peer_rank == my_rank is accepted for MPX_MODE_NONBLOCKING only (MPI's
+   self-send: Isend + Irecv to itself), a one-launch loopback of the path.
+   Check mode (mpx_xfer_opts.check) checksums every received payload in every
+   mode; in the non-blocking loop each in-flight receive lands in a slot of
+   its own (the reference posts all of them into one rx, mpi_perf.c:100,104). */
 int mpx_xfer(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
              void *tx, void *rx, int buff_len, double *sec);
 /* same, with options (checksum mode, timeouts) and full timing */

@@ -1183,8 +1183,14 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     memset(t, 0, sizeof *t);
     if (mode < MPX_MODE_PINGPONG || mode > MPX_MODE_UNIDIR) return fail(MPX_ERR_INVALID, "mode %d", mode);
     if (my_group != 0 && my_group != 1) return fail(MPX_ERR_INVALID, "group %d", my_group);
-    if (my_rank < 0 || my_rank >= ctx->nranks || peer_rank < 0 || peer_rank >= ctx->nranks || my_rank == peer_rank)
+    if (my_rank < 0 || my_rank >= ctx->nranks || peer_rank < 0 || peer_rank >= ctx->nranks)
         return fail(MPX_ERR_INVALID, "ranks %d/%d", my_rank, peer_rank);
+    // a rank paired with itself: only the symmetric non-blocking loop (Isend +
+    // Irecv to itself, MPI's self-send) — the one-kernel loopback every engine
+    // can run on one GPU (RCCL refuses two ranks on one device), and the form
+    // a profiler that serialises dispatches can trace
+    if (my_rank == peer_rank && mode != MPX_MODE_NONBLOCKING)
+        return fail(MPX_ERR_INVALID, "rank %d paired with itself: only the non-blocking loop", my_rank);
     if (iters < 0 || buff_len < 0) return fail(MPX_ERR_INVALID, "iters %d, buff_len %d", iters, buff_len);
     Rank& me = ctx->r[my_rank];
     Rank& peer = ctx->r[peer_rank];

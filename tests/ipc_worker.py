@@ -14,21 +14,27 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 import mpx  # noqa: E402
 
 
+# 8191 / 8192 / 8193: both sides of the cross-GPU LL threshold (ll_max_bytes)
+SIZES = (1, 8, 4097, 8191, 8192, 8193, 65541, 1 << 20)
+
+
 def main():
     d, rank = sys.argv[1], int(sys.argv[2])
     engine = sys.argv[3] if len(sys.argv) > 3 else "kernel"
+    # "cross": rank r on GPU r (the pair moves its bytes over xGMI); else GPU 0
+    dev = rank if len(sys.argv) > 4 and sys.argv[4] == "cross" else 0
     peer = 1 - rank
     group = 1 if rank == 0 else 0
     cap = 1 << 20
     c = mpx.Context(2, engine)
-    tx, rx = c.alloc(0, cap), c.alloc(0, cap)
+    tx, rx = c.alloc(dev, cap), c.alloc(dev, cap)
     c.fill(tx, cap, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, rank, peer, 0))
-    c.attach(rank, 0, tx, rx, cap)
+    c.attach(rank, dev, tx, rx, cap)
     with open(os.path.join(d, f"desc_{rank}.tmp"), "wb") as f:
         f.write(c.export(rank))
     os.rename(os.path.join(d, f"desc_{rank}.tmp"), os.path.join(d, f"desc_{rank}.bin"))
     # my tx checksums, for the peer's expectations
-    sums = {str(n): c.checksum(tx, n) for n in (1, 8, 4097, 65541, cap)}
+    sums = {str(n): c.checksum(tx, n) for n in SIZES}
     with open(os.path.join(d, f"sums_{rank}.tmp"), "w") as f:
         json.dump(sums, f)
     os.rename(os.path.join(d, f"sums_{rank}.tmp"), os.path.join(d, f"sums_{rank}.json"))
@@ -41,7 +47,7 @@ def main():
     peer_sums = json.load(open(os.path.join(d, f"sums_{peer}.json")))
     results = []
     for mode in (mpx.MODE_PINGPONG, mpx.MODE_UNIDIR, mpx.MODE_NONBLOCKING):
-        for n in (1, 8, 4097, 65541, cap):
+        for n in SIZES:
             iters = 300 if mode == mpx.MODE_NONBLOCKING else 9
             t = c.xfer(mode, group, rank, peer, iters, tx, rx, n, check_payload=True,
                        expect=peer_sums[str(n)], expect_ack=peer_sums["1"], timeout_ms=5000)

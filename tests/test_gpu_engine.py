@@ -12,6 +12,7 @@ import pytest
 
 import mpx
 import oracle_py as O
+from pairs import Pairs
 
 pytestmark = pytest.mark.gpu
 
@@ -60,61 +61,8 @@ def test_copy_kernel_matches_oracle(ctx, n):
 
 
 # --------------------------------------------------------------------------
-# loopback pairs
+# loopback pairs (tests/pairs.py; every rank on GPU 0)
 # --------------------------------------------------------------------------
-class Pairs:
-    """`npairs` pairs of loopback ranks on GPU 0: ranks [0,np) are group 1,
-    ranks [np, 2np) group 0, rank k paired with np+k (the -p ppn layout)."""
-
-    def __init__(self, engine, npairs, cap, fill="compat"):
-        self.c = mpx.Context(2 * npairs, engine)
-        self.np = npairs
-        self.cap = cap
-        self.bufs = []
-        for r in range(2 * npairs):
-            tx, rx = self.c.alloc(0, cap), self.c.alloc(0, cap)
-            if fill == "compat":   # mpi_perf.c:244-251: group 0 'a', group 1 'b'
-                self.c.fill(tx, cap, mpx.FILL_BYTE, ord("b") if r < npairs else ord("a"))
-            else:
-                self.c.fill(tx, cap, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, r, 0, 0))
-            self.c.fill(rx, cap, mpx.FILL_BYTE, 0)
-            self.c.attach(r, 0, tx, rx, cap)
-            self.bufs.append((tx, rx))
-
-    def peer(self, r):
-        return r + self.np if r < self.np else r - self.np
-
-    def group(self, r):
-        return 1 if r < self.np else 0
-
-    def expect(self, r, n):
-        tx = self.bufs[self.peer(r)][0]
-        return self.c.checksum(tx, n), self.c.checksum(tx, 1)
-
-    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0, stream=False):
-        ranks = list(range(2 * self.np)) if ranks is None else ranks
-        exp = {r: self.expect(r, n) for r in ranks}
-        out, errs = {}, {}
-
-        def side(r):
-            try:
-                out[r] = self.c.xfer(mode, self.group(r), r, self.peer(r), iters, self.bufs[r][0], self.bufs[r][1],
-                                     n, check_payload=check, expect=exp[r][0], expect_ack=exp[r][1],
-                                     timeout_ms=timeout_ms, nwg=nwg, stream=stream)
-            except mpx.MpxError as e:
-                errs[r] = e
-
-        th = [threading.Thread(target=side, args=(r,)) for r in ranks]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        return out, errs
-
-    def close(self):
-        self.c.close()
-
-
 MODES = [mpx.MODE_PINGPONG, mpx.MODE_NONBLOCKING, mpx.MODE_UNIDIR]
 PAIR_SIZES = [0, 1, 8, 4097, 8192, 8193, 65541, 456131, 4 << 20]
 
@@ -468,3 +416,68 @@ def test_copy_beyond_4gib(ctx):
     finally:
         ctx.free(src)
         ctx.free(dst)
+
+
+# --------------------------------------------------------------------------
+# a rank paired with itself (MPI self-send): the non-blocking loop as ONE
+# launch / one stream — the form every engine, RCCL included, can run on a
+# one-GPU box (RCCL refuses two ranks on one device)
+# --------------------------------------------------------------------------
+def _self_rank(engine, cap):
+    c = mpx.Context(1, engine)
+    tx, rx = c.alloc(0, cap), c.alloc(0, cap)
+    c.fill(tx, cap, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, 0, 0, 7))
+    c.fill(rx, cap, mpx.FILL_BYTE, 0)
+    c.attach(0, 0, tx, rx, cap)
+    if engine == "rccl":
+        c.rccl_init_all()           # a one-rank communicator: send/recv to itself
+    return c, tx, rx
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "rccl"])
+def test_self_pair_nonblocking_every_payload(engine):
+    """Isend + Irecv to itself for every window shape: every payload
+    checksummed (check_iters == iters), the Waitall receives counted and
+    digested on the device, rx = tx at the end; then the same unchecked."""
+    cap = 456131
+    c, tx, rx = _self_rank(engine, cap)
+    try:
+        for n in (0, 1, 4097, 65541, cap):
+            want = c.checksum(tx, n)
+            for iters in (1, 255, 256, 257, 600):
+                t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, n, check_payload=True, expect=want,
+                           timeout_ms=10000)
+                k = iters - iters // 256
+                assert t.check_iters == iters and t.check_failures == 0, (n, iters)
+                assert t.recv_done == k and t.recv_digest == (k * want) & 0xFFFFFFFFFFFFFFFF, (n, iters)
+                assert c.checksum(rx, n) == want
+            t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, 600, tx, rx, n, timeout_ms=10000)
+            assert t.recv_done == 600 - 2 and t.bytes == 2 * n * 600
+        if engine == "rccl":
+            assert t.protocol == 3
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "rccl"])
+def test_self_pair_lost_payload_fails(monkeypatch, engine):
+    monkeypatch.setenv("MPX_TEST_SKIP_PUSH", "3")
+    c, tx, rx = _self_rank(engine, 65541)
+    try:
+        with pytest.raises(mpx.MpxError) as e:
+            c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, 300, tx, rx, 65541, check_payload=True,
+                   expect=c.checksum(tx, 65541), timeout_ms=10000)
+        assert e.value.status == mpx.ERR_CHECK
+    finally:
+        c.close()
+
+
+def test_self_pair_only_for_the_nonblocking_loop():
+    c, tx, rx = _self_rank("kernel", 64)
+    try:
+        for m in (mpx.MODE_PINGPONG, mpx.MODE_UNIDIR):
+            with pytest.raises(mpx.MpxError) as e:
+                c.xfer(m, 1, 0, 0, 1, tx, rx, 8)
+            assert e.value.status == mpx.ERR_INVALID
+    finally:
+        c.close()

@@ -27,7 +27,7 @@ def test_two_process_ipc_pair(tmp_path, engine):
     assert all(p.returncode == 0 for p in procs), outs
     for r in (0, 1):
         res = json.load(open(tmp_path / f"result_{r}.json"))
-        assert len(res) == 15
+        assert len(res) == 3 * 8
         for x in res:
             assert x["final_rx_ok"], (r, x)
             # every payload checked, the non-blocking loop's 300 included
