@@ -20,7 +20,7 @@ constexpr int kStageMaxBytes = 60 << 10; // LDS-staged tx chunk per workgroup, m
                                          // (under a 64 KiB per-workgroup LDS limit)
 
 // Protocol ids reported in mpx_timing.protocol
-enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4 };
+enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4, kProtoCopySteps = 5 };
 
 // One rank's receive mailbox, in that rank's HBM (uncached / fine-grained so a
 // poll sees stores that arrive over xGMI).  Written ONLY by the peers, polled
@@ -141,6 +141,15 @@ inline int bulk_nwg(long long len, bool same_device) {
 // Launchers implemented in mpx_kernels.hip
 hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s);
 hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int* grid_out);
+// all `iters` copies in one launch with a grid barrier between steps; *bar
+// must be 0 at launch
+constexpr int kCopyStepsMaxGrid = 1024;   // 4 workgroups per CU: always co-resident
+// copies up to 4 MiB run as k_copy_steps: faster than a launch per copy
+// there (4 MiB 2.95 vs 3.18 us), slower from 8 MiB (3.66 vs 3.31 us;
+// profiles/r02_copy_steps_variants.jsonl)
+constexpr size_t kCopyStepsDefaultMax = (size_t)4 << 20;
+hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
+                             int* grid_out);
 hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s);
 hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s);
 hipError_t launch_signal(u64* flag, const u64* base, u64 value, hipStream_t s);

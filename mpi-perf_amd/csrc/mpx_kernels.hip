@@ -118,6 +118,63 @@ __global__ __launch_bounds__(kBlock) void k_copy(const v4u* __restrict__ src, v4
 }
 
 // ---------------------------------------------------------------------------
+// k_copy_steps: all `iters` copies dst[0:n) = src[0:n) of one mpx_copy call in
+// ONE launch (the reference's loop, mpi_perf.c:70, run on the device like
+// k_xfer runs the pair loop).  Below a few MiB a launch of k_copy costs
+// 2.1-2.5 us whatever it moves (profiles/r01_cfg2_copy_sweep.jsonl), so the
+// sweep's small sizes measured dispatch, not memory.  Every lane owns the
+// same 16-B units every step (grid-stride, U = ceil(n16 / (grid*256)) per
+// lane); between steps a grid barrier: one lane per workgroup counts in
+// (optionally after draining its stores) and waits for the whole grid, so
+// step s+1's loads start only after every store of
+// step s was issued — back-to-back copies, not an overlapped pipeline.  The
+// grid (<= 4 workgroups per CU, 12 VGPRs) is always co-resident.
+// ---------------------------------------------------------------------------
+template <bool XCD>
+__global__ __launch_bounds__(kBlock) void k_copy_steps(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n16,
+                                                      unsigned tail, int iters, u64* bar, int drain) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const size_t first = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const u64 g = gridDim.x;
+    // XCD = true: two-level arrival.  Workgroups are dispatched round-robin
+    // over the 8 XCDs, so workgroup b counts in on its XCD's counter
+    // bar[16 * (1 + b % 8)] (8 counters, 128 B apart, in parallel instead of
+    // one hot word); the last arriver of each XCD then counts that XCD in on
+    // bar[0].
+    const int x = (int)(blockIdx.x & 7);
+    const u64 nx = (g - (u64)x + 7) / 8;            // workgroups on this XCD
+    const u64 groups = g < 8 ? g : 8;
+    for (int s = 0; s < iters; ++s) {
+        for (size_t i = first; i < n16; i += stride)
+            __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+        if (blockIdx.x == 0 && threadIdx.x < tail) {
+            const unsigned char* s8 = reinterpret_cast<const unsigned char*>(src + n16);
+            reinterpret_cast<unsigned char*>(dst + n16)[threadIdx.x] = s8[threadIdx.x];
+        }
+        if (s + 1 == iters) break;
+        if (drain) drain_stores();
+        __syncthreads();
+        if (g == 1) continue;                       // one workgroup: __syncthreads is the barrier
+        if (threadIdx.x == 0) {
+            u64 want;
+            if constexpr (XCD) {
+                const u64 old = __hip_atomic_fetch_add(bar + 16 * (1 + x), 1ull, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (old + 1 == nx * (u64)(s + 1))
+                    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                want = groups * (u64)(s + 1);
+            } else {
+                __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                want = g * (u64)(s + 1);
+            }
+            while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+                __builtin_amdgcn_s_sleep(1);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_fill
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_fill(unsigned char* p, size_t n, int pattern, u64 arg) {
@@ -839,6 +896,29 @@ hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int*
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const v4u*>(src),
                        reinterpret_cast<v4u*>(dst), n16, tail);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
+                             int* grid_out) {
+    // Defaults from the A/B (profiles/r02_copy_steps_variants.jsonl): up to
+    // 1 MiB 64 workgroups and one hot counter (fewer arrivals beat more
+    // lanes: 1 MiB 2.08 us vs 2.40 with 256), above that 256 workgroups with
+    // the per-XCD counters; no store drain before arrival (the barrier orders
+    // issue, not acknowledgement: -0.05..0.1 us per step).
+    // MPX_COPY_STEPS="grid_cap:xcd:drain" overrides (A/B knobs, read per call).
+    int cap = n <= ((size_t)1 << 20) ? 64 : 256, xcd = cap > 64, drain = 0;
+    if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d", &cap, &xcd, &drain);
+    if (cap < 1 || cap > kCopyStepsMaxGrid) cap = kCopyStepsMaxGrid;
+    const size_t n16 = n / 16;
+    size_t grid = (n16 + kBlock - 1) / kBlock;
+    if (grid > (size_t)cap) grid = (size_t)cap;
+    if (grid < 1) grid = 1;
+    if (grid_out) *grid_out = (int)grid;
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
+    hipLaunchKernelGGL(xcd ? k_copy_steps<true> : k_copy_steps<false>, dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       reinterpret_cast<const v4u*>(src), reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters,
+                       bar, drain);
     return hipGetLastError();
 }
 

@@ -173,7 +173,8 @@ int util_stream(mpx_ctx* ctx, int dev, hipStream_t* s) {
     hipStream_t st;
     HIPCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     u64* tmp;
-    HIPCK(hipMalloc(&tmp, 64));
+    // [0] checksum sum; [16 ..) k_copy_steps' barrier: 9 counters 128 B apart
+    HIPCK(hipMalloc(&tmp, 16 * 10 * sizeof(u64)));
     ctx->dev_stream[dev] = st;
     ctx->dev_tmp[dev] = tmp;
     *s = st;
@@ -266,6 +267,13 @@ unsigned char* slot_ptr(const Rank& rk, int j, int iters, int slots, long long l
     return s == 0 ? rk.rx : rk.ring + (long long)(s - 1) * len;
 }
 
+// Largest copy whose iterations run in one k_copy_steps launch
+// (MPX_COPY_STEPS_MAX bytes, read per call for A/B sweeps; 0 = never).
+size_t copy_steps_max() {
+    const char* v = getenv("MPX_COPY_STEPS_MAX");
+    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyStepsDefaultMax;
+}
+
 // the receives the reference's non-blocking loop completes (Waitall) for
 // `iters` iterations: slot 255 of each full window is never waited for
 // (mpi_perf.c:95-124)
@@ -281,6 +289,11 @@ int skip_push_knob() {
     return v ? atoi(v) : 0;
 }
 
+bool plain_streams() {
+    const char* kind = getenv("MPX_STREAM");
+    return kind && !strcmp(kind, "plain");
+}
+
 // A rank's stream must own its hardware queue.  The two halves of a pair
 // are co-dependent persistent kernels; when both ranks live on one GPU and
 // HIP multiplexes their streams onto one of its GPU_MAX_HW_QUEUES shared
@@ -289,24 +302,48 @@ int skip_push_knob() {
 // rank stream is created with a mask that enables all CUs.
 // MPX_STREAM=plain falls back to an ordinary non-blocking stream.
 //
-// Destroying a CU-masked stream was observed to leave later HIP calls of the
-// process hanging (gfx950 / ROCm 7.2), so these streams are never destroyed:
-// finalize returns them to a process-wide pool and the next attach reuses them.
-std::mutex g_pool_mu;
-std::map<int, std::vector<hipStream_t>> g_stream_pool;
-
-bool plain_streams() {
-    const char* kind = getenv("MPX_STREAM");
-    return kind && !strcmp(kind, "plain");
+// Teardown rule (gfx950 / ROCm 7.2, isolated with tools/stream_teardown.hip,
+// profiles/r02_stream_teardown.txt): a CU-masked stream owns a dedicated HSA
+// queue that hipStreamDestroy frees.  hipFree of memory whose last use was a
+// kernel on such a destroyed stream leaves the runtime waiting on that queue:
+// the next queue creation, stream destruction or the process exit hangs
+// ("a0 m0 k0.0 d0 f0" hangs at exit; "a0 m0 k0.0 f0 d0" is fine; freeing a
+// buffer no kernel touched is fine either way).  Even with every allocation
+// of a context freed before its streams are destroyed, a long-lived process
+// that creates and finalizes contexts one after another hung in a later
+// context's first hipMalloc/launch (the -m gpu suite, ~60 contexts in:
+// profiles/r02_stream_destroy_suite_hang.txt).  So rank streams are
+// process-lifetime objects, like the runtime's own queues: mpx_finalize
+// drains them, frees every allocation of the context, and returns them to a
+// per-device pool that later contexts reuse; an exit handler destroys the
+// pool when no context is alive (all memory they touched is freed by then —
+// the safe order).  No HIP call may run later than that at exit: under
+// rocprofv3 the tool finalizes in its own exit handler, and a HIP call after
+// it (the runtime's exit teardown of leaked streams in round 1, or this pool
+// destroyed from a library destructor) ends in SIGSEGV in __cxa_finalize
+// (profiles/r02_prof_n2_exit.txt).  The handler is registered with atexit()
+// when the first rank stream is created, i.e. after the tool's, so it runs
+// before it.
+struct StreamPool {
+    std::mutex mu;
+    std::map<int, std::vector<hipStream_t>> idle;    // per device
+    std::vector<std::pair<int, hipStream_t>> all;    // every stream ever created
+    int live_contexts = 0;
+};
+StreamPool& pool() {
+    static StreamPool* p = new StreamPool;   // never destroyed: no static-destructor ordering
+    return *p;
 }
+
+void destroy_stream_pool();
 
 void release_rank_stream(int dev, hipStream_t s) {
     if (plain_streams()) {
         (void)hipStreamDestroy(s);
         return;
     }
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_stream_pool[dev].push_back(s);
+    std::lock_guard<std::mutex> lk(pool().mu);
+    pool().idle[dev].push_back(s);
 }
 
 int create_rank_stream(int dev, hipStream_t* s) {
@@ -315,8 +352,8 @@ int create_rank_stream(int dev, hipStream_t* s) {
         return MPX_OK;
     }
     {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        auto& v = g_stream_pool[dev];
+        std::lock_guard<std::mutex> lk(pool().mu);
+        auto& v = pool().idle[dev];
         if (!v.empty()) {
             *s = v.back();
             v.pop_back();
@@ -328,7 +365,28 @@ int create_rank_stream(int dev, hipStream_t* s) {
     const int words = (prop.multiProcessorCount + 31) / 32;
     std::vector<uint32_t> mask((size_t)words, 0xffffffffu);
     HIPCK(hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask.data()));
+    static std::once_flag registered;
+    std::call_once(registered, [] { atexit(destroy_stream_pool); });
+    std::lock_guard<std::mutex> lk(pool().mu);
+    pool().all.emplace_back(dev, *s);
     return MPX_OK;
+}
+
+// exit handler (registered at the first rank stream, see above)
+void destroy_stream_pool() {
+    StreamPool& p = pool();
+    std::lock_guard<std::mutex> lk(p.mu);
+    if (p.live_contexts != 0 || p.all.empty()) return;   // a context still owns memory they touched
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (auto& ds : p.all) {
+        (void)hipSetDevice(ds.first);
+        (void)hipStreamSynchronize(ds.second);
+        (void)hipStreamDestroy(ds.second);
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    p.all.clear();
+    p.idle.clear();
 }
 
 bool same_device(const Rank& a, const Rank& b) {
@@ -863,6 +921,10 @@ int mpx_init(int nranks, int engine, mpx_ctx** out) {
     mpx_ctx* c = new mpx_ctx;
     c->nranks = nranks;
     c->engine = engine;
+    {
+        std::lock_guard<std::mutex> lk(pool().mu);
+        ++pool().live_contexts;
+    }
     *out = c;
     return MPX_OK;
 }
@@ -873,9 +935,8 @@ int mpx_init(int nranks, int engine, mpx_ctx** out) {
 int mpx_finalize(mpx_ctx* ctx) {
     if (!ctx) return fail(MPX_ERR_INVALID, "ctx is NULL");
     // Teardown order matters: every stream is drained and every allocation
-    // freed BEFORE any stream is destroyed — hipFree after destroying a
-    // CU-masked stream (create_rank_stream) was observed to hang on gfx950 /
-    // ROCm 7.2.
+    // freed, then the rank streams go back to the process pool (the teardown
+    // rule above create_rank_stream).
     for (int i = 0; i < MPX_MAX_RANKS; ++i) {
         Rank& rk = ctx->r[i];
         if (rk.comm) (void)ncclCommDestroy(rk.comm);
@@ -929,6 +990,10 @@ int mpx_finalize(mpx_ctx* ctx) {
     }
     DBG("finalize: done\n");
     delete ctx;
+    {
+        std::lock_guard<std::mutex> lk(pool().mu);
+        --pool().live_contexts;
+    }
     return MPX_OK;
 }
 
@@ -1029,9 +1094,17 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     HIPCK(hipEventCreate(&e0));
     HIPCK(hipEventCreate(&e1));
     int grid = 0;
+    // copies of <= copy_steps_max() bytes run all iterations in one launch
+    // (k_copy_steps: dispatch-bound sizes); larger ones one k_copy launch each
+    const bool steps = n && iters > 1 && n <= copy_steps_max();
+    u64* bar = ctx->dev_tmp[dev] + 16;
+    if (steps) HIPCK(hipMemsetAsync(bar, 0, 9 * 16 * sizeof(u64), s));   // global + 8 per-XCD counters
     const double t0 = now_s();
     HIPCK(hipEventRecord(e0, s));
-    for (int i = 0; i < iters && n; ++i) HIPCK(launch_copy(dst, src, n, s, &grid));
+    if (steps)
+        HIPCK(launch_copy_steps(dst, src, n, iters, bar, s, &grid));
+    else
+        for (int i = 0; i < iters && n; ++i) HIPCK(launch_copy(dst, src, n, s, &grid));
     HIPCK(hipEventRecord(e1, s));
     HIPCK(hipEventSynchronize(e1));
     t->wall_s = now_s() - t0;
@@ -1041,9 +1114,9 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     (void)hipEventDestroy(e1);
     t->device_s = ms * 1e-3;
     t->bytes = (uint64_t)n * (uint64_t)iters;
-    t->launches = n ? iters : 0;
+    t->launches = !n ? 0 : steps ? 1 : iters;
     t->nwg = grid;
-    t->protocol = kProtoCopy;
+    t->protocol = steps ? kProtoCopySteps : kProtoCopy;
     return MPX_OK;
 }
 

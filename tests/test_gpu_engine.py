@@ -42,6 +42,32 @@ def test_fill_and_checksum_match_oracle(ctx, n, pattern):
         ctx.free(b)
 
 
+@pytest.mark.parametrize("iters", [1, 7])
+@pytest.mark.parametrize("n", [1, 4096 + 5, (1 << 20) + 3, (4 << 20), (4 << 20) + 16, (8 << 20) + 1])
+def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
+    """k_copy_steps (all copies in one launch, grid barrier between steps) at
+    the grid-size classes of its defaults (one workgroup; <= 64 with one
+    counter; 256 with the per-XCD counters) and both sides of the 4 MiB
+    threshold, plus every A/B knob combination at 1 MiB: output against the
+    oracle's pattern, nothing written past the end."""
+    key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
+    src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
+    try:
+        ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
+        variants = [None] + (["64:0:1", "256:1:1", "1024:1:0", "1:0:0"] if n == (1 << 20) + 3 else [])
+        for v in variants:
+            if v:
+                monkeypatch.setenv("MPX_COPY_STEPS", v)
+            ctx.fill(dst, n + 64, mpx.FILL_BYTE, 0xEE)
+            t = ctx.copy(0, dst, src, n, iters)
+            assert ctx.checksum(dst, n) == O.pattern_checksum(n, mpx.FILL_SPLITMIX, key), v
+            assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
+            assert t.bytes == n * iters
+    finally:
+        ctx.free(src)
+        ctx.free(dst)
+
+
 @pytest.mark.parametrize("n", SIZES)
 def test_copy_kernel_matches_oracle(ctx, n):
     key = mpx.pattern_key(mpx.PATTERN_SEED, 0, 0, n & 0xFFFF)
@@ -54,7 +80,11 @@ def test_copy_kernel_matches_oracle(ctx, n):
         # nothing written past the end
         assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
         assert t.bytes == 2 * n
-        assert t.launches == (2 if n else 0)
+        # both copies in one k_copy_steps launch up to 4 MiB, a launch each above
+        steps = 0 < n <= (4 << 20)
+        assert t.launches == (1 if steps else 2 if n else 0)
+        if n:
+            assert mpx.PROTOCOLS[t.protocol] == ("copy_steps" if steps else "copy")
     finally:
         ctx.free(src)
         ctx.free(dst)
