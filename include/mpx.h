@@ -100,7 +100,9 @@ typedef struct mpx_timing {
     int32_t launches;         /* kernels / copies issued for the loop          */
     int32_t nwg;              /* workgroups of the data push (kernel engine)   */
     int32_t protocol;         /* 0 = LL granules, 1 = bulk+flags, 2 = SDMA,
-                                 3 = RCCL, 4 = local copy kernel               */
+                                 3 = RCCL, 4 = local copy kernel (a launch per
+                                 copy), 5 = local copy, all iterations in one
+                                 launch (k_copy_steps)                          */
     int32_t check_failures;   /* iterations whose payload checksum mismatched  */
     uint64_t check_iters;     /* iterations whose payload was checksummed      */
     /* receive accounting, as the reference's loop completes receives: every
@@ -203,6 +205,14 @@ int mpx_xfer(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, i
 /* same, with options (checksum mode, timeouts) and full timing */
 int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
                 void *tx, void *rx, int buff_len, const mpx_xfer_opts *opts, mpx_timing *t);
+
+/* Build, outside any timed region, what a later mpx_xfer_ex with the same
+   (mode, group, ranks, iters, buff_len, opts) would otherwise build on its
+   first call: the SDMA engine's graph-captured loop chunks.  The reference's
+   timer brackets only the loop (mpi_perf.c:501-533), so hosts call this
+   before their barrier (mpi_perf.c:499).  A no-op for the other engines. */
+int mpx_xfer_prepare(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
+                     int buff_len, const mpx_xfer_opts *opts);
 
 /* MPI_Barrier analogue (mpi_perf.c:499,557,579) for the threads of ONE
    process: blocks until `nthreads` callers have entered with the same ctx.

@@ -1312,6 +1312,32 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     return MPX_OK;
 }
 
+int mpx_xfer_prepare(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, int buff_len,
+                     const mpx_xfer_opts* opts) {
+    if (!ctx) return fail(MPX_ERR_INVALID, "NULL argument");
+    if (mode < MPX_MODE_PINGPONG || mode > MPX_MODE_UNIDIR) return fail(MPX_ERR_INVALID, "mode %d", mode);
+    if (my_rank < 0 || my_rank >= ctx->nranks || peer_rank < 0 || peer_rank >= ctx->nranks)
+        return fail(MPX_ERR_INVALID, "ranks %d/%d", my_rank, peer_rank);
+    if (iters < 0 || buff_len < 0) return fail(MPX_ERR_INVALID, "iters %d, buff_len %d", iters, buff_len);
+    Rank& me = ctx->r[my_rank];
+    Rank& peer = ctx->r[peer_rank];
+    if (!me.local) return fail(MPX_ERR_STATE, "rank %d is not attached in this process", my_rank);
+    // only the SDMA engine builds anything per (mode, side, peer, B): the
+    // graph-captured chunks run_sdma replays (not used in check mode)
+    if (ctx->engine != MPX_ENGINE_SDMA || (opts && opts->check) || !sdma_graphs_enabled() || iters < kSdmaGraphMin)
+        return MPX_OK;
+    if (!peer.local && !peer.imported) return fail(MPX_ERR_STATE, "peer rank %d is unknown", peer_rank);
+    DeviceGuard g(me.dev);
+    HIPCK(g.err);
+    const u64 tmo = timeout_ticks(opts);
+    hipGraphExec_t x = nullptr;
+    if (iters / kSdmaChunk > 0)
+        TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, my_group, buff_len, tmo, kSdmaChunk, &x));
+    if (iters % kSdmaChunk >= kSdmaGraphMin)
+        TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, my_group, buff_len, tmo, iters % kSdmaChunk, &x));
+    return MPX_OK;
+}
+
 int mpx_xfer(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, void* tx, void* rx,
              int buff_len, double* sec) {
     mpx_timing t;

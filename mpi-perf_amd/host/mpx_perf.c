@@ -245,6 +245,10 @@ static void *rank_main(void *arg)
                 xo.expect_ack = txsum1_of[peer];
             }
 
+            /* SDMA engine: capture this (mode, peer, B)'s graph chunks now, not
+               inside the timed call (the reference's timer brackets only the
+               loop, mpi_perf.c:501-533) */
+            if (!opt.use_dotnet) MPX_CHECK(mpx_xfer_prepare(ctx, xfer_mode(), group, r, peer, opt.iters, B, &xo));
             barrier(); /* MPI_Barrier, mpi_perf.c:499 */
             const double t_start = wtime();
             mpx_timing tm;

@@ -93,6 +93,8 @@ _SIGS = {
                            C.c_int, C.POINTER(C.c_double)]),
     "mpx_xfer_ex": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                               C.c_int, C.POINTER(XferOpts), C.POINTER(Timing)]),
+    "mpx_xfer_prepare": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.POINTER(XferOpts)]),
     "mpx_barrier": (C.c_int, [C.c_void_p, C.c_int]),
     "mpx_rccl_get_unique_id": (C.c_int, [C.c_void_p]),
     "mpx_rccl_init_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
@@ -229,6 +231,13 @@ class Context:
                                 C.c_void_p(rx.ptr), length, C.byref(o), C.byref(t))
         check(st, "mpx_xfer_ex")
         return t
+
+    def prepare(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, length: int,
+                timeout_ms: int = 0) -> None:
+        """mpx_xfer_prepare: build the SDMA engine's graph chunks before timing"""
+        o = XferOpts(timeout_ms=timeout_ms)
+        check(self.L.mpx_xfer_prepare(self.h, mode, group, my_rank, peer_rank, iters, length, C.byref(o)),
+              "mpx_xfer_prepare")
 
     def rccl_init_all(self) -> None:
         check(self.L.mpx_rccl_init_all(self.h), "mpx_rccl_init_all")

@@ -45,6 +45,7 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
     res = run(world, "ok", tmp_path)
     rounds = all_pairs_rounds(world)
     n, iters, steps, warmup = 4096, 7, 5, 2
+    warmup = max(warmup, world - 1)          # pairs_bench warms every round up at least once
     for d in res:
         r = d["rank"]
         assert d["engine_used"] == "kernel"
@@ -135,6 +136,18 @@ def test_kernel_validation_failure_falls_back_to_sdma_with_a_label(world, tmp_pa
         inits = [i for i, x in enumerate(d["log"]) if x[0] == "init"]
         closes = [i for i, x in enumerate(d["log"]) if x[0] == "close" and x[1] == "kernel"]
         assert closes and inits[1] > closes[0]
+        # SDMA: every round's graph chunks are built (mpx_xfer_prepare) before
+        # the first untimed step, and every round gets a warm-up step, so no
+        # capture lands inside the timed steps (bench.py)
+        rounds = all_pairs_rounds(world)
+        log = d["log"]
+        steps_at = [i for i, x in enumerate(log) if x[0] == "xfer" and x[1] == "sdma" and not x[8] and x[6] == 7]
+        prep = [(i, x) for i, x in enumerate(log) if x[0] == "prepare" and x[1] == "sdma"]
+        assert {(x[3], x[5]) for _, x in prep} == {round_role(rounds, rd, d["rank"]) for rd in range(world - 1)}
+        assert all(i < steps_at[0] for i, _ in prep)
+        warm = max(2, world - 1)
+        assert [(x[3], x[5]) for x in (log[i] for i in steps_at[:warm])] == \
+            [round_role(rounds, s % (world - 1), d["rank"]) for s in range(warm)]
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -146,6 +159,7 @@ def test_push_tuning_agrees_across_ranks(world, tmp_path):
     res = run(world, "tune", tmp_path)
     rounds = all_pairs_rounds(world)
     n, warmup, steps = 65536, 2, 5
+    warmup = max(warmup, world - 1)          # pairs_bench warms every round up at least once
     ms = {16: 5, 32: 7, 64: 3, 128: 4, 256: 6}
     want = {}
     for w in (16, 32, 64, 128, 256):

@@ -43,11 +43,11 @@ def test_fill_and_checksum_match_oracle(ctx, n, pattern):
 
 
 @pytest.mark.parametrize("iters", [1, 7])
-@pytest.mark.parametrize("n", [1, 4096 + 5, (1 << 20) + 3, (4 << 20), (4 << 20) + 16, (8 << 20) + 1])
+@pytest.mark.parametrize("n", [1, 4096 + 5, (1 << 20) + 3, (2 << 20), (2 << 20) + 16, (8 << 20) + 1])
 def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
     """k_copy_steps (all copies in one launch, grid barrier between steps) at
     the grid-size classes of its defaults (one workgroup; <= 64 with one
-    counter; 256 with the per-XCD counters) and both sides of the 4 MiB
+    counter; 256 with the per-XCD counters) and both sides of the 2 MiB
     threshold, plus every A/B knob combination at 1 MiB: output against the
     oracle's pattern, nothing written past the end."""
     key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
@@ -80,8 +80,8 @@ def test_copy_kernel_matches_oracle(ctx, n):
         # nothing written past the end
         assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
         assert t.bytes == 2 * n
-        # both copies in one k_copy_steps launch up to 4 MiB, a launch each above
-        steps = 0 < n <= (4 << 20)
+        # both copies in one k_copy_steps launch up to 2 MiB, a launch each above
+        steps = 0 < n <= (2 << 20)
         assert t.launches == (1 if steps else 2 if n else 0)
         if n:
             assert mpx.PROTOCOLS[t.protocol] == ("copy_steps" if steps else "copy")
