@@ -51,6 +51,8 @@ struct Status {
     // non-blocking loop, mpi_perf.c:75,79,110-111,122-123,137,141)
     u64 recv_done;          // receives completed
     u64 recv_digest;        // check mode: sum of their finished checksums
+    u64 seen, want;         // stream engines: flag value seen / awaited by the
+                            // wait that timed out (diagnostics)
 };
 
 // Device scratch words of a rank (zeroed per kernel-engine call, [0..3]):

@@ -233,13 +233,21 @@ __global__ void k_signal(u64* flag, const u64* base, u64 v) {
     if (threadIdx.x == 0) st_sys(flag, rel(base, v));
 }
 
+// A wait of a call whose earlier wait already gave up returns at once: the
+// stream then drains in microseconds instead of one deadline per remaining
+// wait (a peer that stopped — e.g. its process exited on an error — would
+// otherwise hold this stream, and the exit of this process, for deadline x
+// the hundreds of waits a checked loop enqueues).
 __global__ void k_wait(const u64* flag, const u64* base, u64 v, Status* st, u64 timeout_ticks) {
     if (threadIdx.x != 0) return;
+    if (__hip_atomic_load(&st->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
     const u64 want = rel(base, v);
     const u64 t0 = now_ticks();
-    u64 spins = 0;
-    while (ld_sys(flag) < want) {
+    u64 spins = 0, seen;
+    while ((seen = ld_sys(flag)) < want) {
         if ((++spins & 255) == 0 && now_ticks() - t0 > timeout_ticks) {
+            st->seen = seen;   // diagnostics, read by the host after the stream drains
+            st->want = want;
             __hip_atomic_store(&st->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }

@@ -775,7 +775,9 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
     if (__atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE)) {
         me.broken = true;
-        return fail(MPX_ERR_TIMEOUT, "rank %d <- rank %d: SDMA-engine wait timed out", my_rank, peer_rank);
+        return fail(MPX_ERR_TIMEOUT, "rank %d <- rank %d: SDMA-engine wait timed out (flag %llu, awaited %llu; "
+                    "sequence bases tx %llu rx %llu, mode %d, %lld B, %d iterations)", my_rank, peer_rank,
+                    me.status->seen, me.status->want, txs0, rxs0, mode, len, iters);
     }
     me.tx_seq[peer_rank] += (u64)iters;
     me.rx_seq[peer_rank] += (u64)iters;

@@ -1,4 +1,5 @@
-"""Pair schedules (Python mirror of mpi-perf_amd/host/mpx_sched.c).
+"""Pair schedules (Python mirror of mpxh_pairing / mpxh_round_role in
+mpi-perf_amd/host/mpx_host.c).
 
 pairing_from_groups(): the reference's group/peer rule (mpi_perf.c:447-450
 Comm_split keyed by world rank; :225-233 first other-group rank with the same

@@ -100,6 +100,42 @@ def test_all_pairs_rounds_cover_every_pair_once(H, n):
     assert H.mpxh_round_pairs(3, 0, (C.c_int * 4)()) == -1
 
 
+@pytest.mark.parametrize("mode", ["pingpong", "nonblocking", "unidir"])
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_every_round_is_a_reference_run_with_ppn_half(H, n, mode):
+    """round r of the N-GPU schedule is the reference's own run
+    with ppn = N/2 on two hosts (golden <mode>_p<N/2>_*: ranks [0, N/2) are
+    group 1, rank l's peer is l +- N/2, mpi_perf.c:225-233,447-450) under the
+    rank relabelling sigma_r(l) = order_r[l] for l < N/2 and
+    order_r[3N/2 - 1 - l] for l >= N/2, where order_r is the circle method's
+    seating of round r (rank 0 fixed, the rest rotated r places:
+    mpxh_round_pairs pairs seat k with seat N-1-k).  The reference run's
+    group / peer of every logical rank, mapped through sigma_r, must be what
+    mpxh_round_role gives the GPU rank sigma_r(l) in round r."""
+    ref = CASES[f"{mode}_p{n // 2}_b8_i10"]
+    info = {d["rank"]: d for d in ref["info"]}
+    assert sorted(info) == list(range(n))
+    for r in range(n - 1):
+        pairs = (C.c_int * n)()
+        assert H.mpxh_round_pairs(n, r, pairs) == n // 2
+        # seat k of round r: the G1 end of pair k for k < N/2, the G0 end of
+        # pair N-1-k otherwise
+        order = [0] * n
+        for k in range(n // 2):
+            order[k], order[n - 1 - k] = pairs[2 * k], pairs[2 * k + 1]
+        sigma = [order[l] if l < n // 2 else order[3 * n // 2 - 1 - l] for l in range(n)]
+        assert sorted(sigma) == list(range(n))                        # a relabelling
+        for l in range(n):
+            grp, peer = C.c_int(), C.c_int()
+            assert H.mpxh_round_role(n, r, sigma[l], C.byref(grp), C.byref(peer)) == 0
+            assert (grp.value, peer.value) == (info[l]["group"], sigma[info[l]["peer"]]), (r, l)
+        # the round's senders (record writers, mpi_perf.c:545) are sigma of the
+        # reference's record ranks
+        writers = sorted({rec["rank"] for rec in ref["records"]})
+        assert writers == list(range(n // 2))
+        assert sorted(sigma[w] for w in writers) == sorted(pairs[2 * k] for k in range(n // 2))
+
+
 @pytest.mark.parametrize("name", [c["name"] for c in G["cases"] if c["records"]][:20])
 def test_record_format_matches_reference(H, name):
     c = CASES[name]
