@@ -130,6 +130,12 @@ __global__ __launch_bounds__(kBlock) void k_copy(const v4u* __restrict__ src, v4
 // step s was issued — back-to-back copies, not an overlapped pipeline.  The
 // grid (<= 4 workgroups per CU, 12 VGPRs) is always co-resident.
 // ---------------------------------------------------------------------------
+// Each lane issues the loads of up to kCopyStepsBatch of its units before
+// the first store, so a step costs about one memory latency per batch, not
+// one per unit (the grid is sized to give every lane <= one batch per step
+// below 1 MiB).
+constexpr int kCopyStepsBatch = 8;
+
 template <bool XCD>
 __global__ __launch_bounds__(kBlock) void k_copy_steps(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n16,
                                                       unsigned tail, int iters, u64* bar, int drain) {
@@ -144,9 +150,19 @@ __global__ __launch_bounds__(kBlock) void k_copy_steps(const v4u* __restrict__ s
     const int x = (int)(blockIdx.x & 7);
     const u64 nx = (g - (u64)x + 7) / 8;            // workgroups on this XCD
     const u64 groups = g < 8 ? g : 8;
+    const bool one_unit = n16 <= stride;   // at most one unit per lane: no batch
     for (int s = 0; s < iters; ++s) {
-        for (size_t i = first; i < n16; i += stride)
-            __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+        if (one_unit) {
+            if (first < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(src + first), dst + first);
+        } else for (size_t base = first; base < n16; base += kCopyStepsBatch * stride) {
+            v4u r[kCopyStepsBatch];
+#pragma unroll
+            for (int u = 0; u < kCopyStepsBatch; ++u)
+                if (base + u * stride < n16) r[u] = __builtin_nontemporal_load(src + base + u * stride);
+#pragma unroll
+            for (int u = 0; u < kCopyStepsBatch; ++u)
+                if (base + u * stride < n16) __builtin_nontemporal_store(r[u], dst + base + u * stride);
+        }
         if (blockIdx.x == 0 && threadIdx.x < tail) {
             const unsigned char* s8 = reinterpret_cast<const unsigned char*>(src + n16);
             reinterpret_cast<unsigned char*>(dst + n16)[threadIdx.x] = s8[threadIdx.x];
@@ -909,17 +925,23 @@ hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int*
 
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
                              int* grid_out) {
-    // Defaults from the A/B (profiles/r02_copy_steps_variants.jsonl): up to
-    // 1 MiB 64 workgroups and one hot counter (fewer arrivals beat more
-    // lanes: 1 MiB 2.08 us vs 2.40 with 256), above that 256 workgroups with
-    // the per-XCD counters; no store drain before arrival (the barrier orders
-    // issue, not acknowledgement: -0.05..0.1 us per step).
-    // MPX_COPY_STEPS="grid_cap:xcd:drain" overrides (A/B knobs, read per call).
-    int cap = n <= ((size_t)1 << 20) ? 64 : 256, xcd = cap > 64, drain = 0;
-    if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d", &cap, &xcd, &drain);
+    // Defaults from the A/Bs: at most 64 workgroups and one hot counter
+    // (fewer arrivals beat more lanes: 1 MiB 2.08 us vs 2.40 with 256,
+    // profiles/r02_copy_steps_variants.jsonl); no store drain before arrival
+    // (the barrier orders issue, not acknowledgement: -0.05..0.1 us per step);
+    // the grid sized for `upl` 16-B units per lane per step, all of a lane's
+    // loads in flight at once: 1 up to 128 KiB, 4 at 256-512 KiB, 8 at
+    // 1 MiB, 2 above (profiles/r02_copy_steps_upl.jsonl: 512 KiB 2.14 ->
+    // 1.82 us, 1 MiB 2.20 -> 2.02 against one unit per lane; below 256 KiB
+    // the two bench sweeps disagreed by more than the A/B's difference).
+    // MPX_COPY_STEPS="grid_cap:xcd:drain:upl" overrides (A/B knobs, read per call).
+    int cap = 64, xcd = 0, drain = 0;
+    int upl = n <= ((size_t)128 << 10) ? 1 : n <= ((size_t)512 << 10) ? 4 : n <= ((size_t)1 << 20) ? 8 : 2;
+    if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d:%d", &cap, &xcd, &drain, &upl);
     if (cap < 1 || cap > kCopyStepsMaxGrid) cap = kCopyStepsMaxGrid;
+    if (upl < 1) upl = 1;
     const size_t n16 = n / 16;
-    size_t grid = (n16 + kBlock - 1) / kBlock;
+    size_t grid = (n16 + (size_t)kBlock * upl - 1) / ((size_t)kBlock * upl);
     if (grid > (size_t)cap) grid = (size_t)cap;
     if (grid < 1) grid = 1;
     if (grid_out) *grid_out = (int)grid;

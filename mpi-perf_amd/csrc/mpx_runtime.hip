@@ -377,16 +377,39 @@ void destroy_stream_pool() {
     StreamPool& p = pool();
     std::lock_guard<std::mutex> lk(p.mu);
     if (p.live_contexts != 0 || p.all.empty()) return;   // a context still owns memory they touched
+    // The runtime finishes a drained stream's last commands on its HSA event
+    // thread (completion callbacks) slightly after hipStreamSynchronize
+    // returns.  Destroying the stream under a callback still in flight left
+    // the runtime's own exit teardown (HIP's static destructors, in
+    // __cxa_finalize) waiting forever on that thread: mpx_perf -e sdma -x 1
+    // -c 1, two ranks on GPU 0, stalled after its last line in 2 of 4 suite
+    // runs and in the first attempt of tools/gpu_exit_hang.sh (all-thread
+    // stacks: profiles/r02_exit_stall.txt).  With 50 ms between the drain
+    // and the destroys, 0 of 6 attempts stalled; with the streams left to the
+    // runtime, 0 of 6 (but then the runtime destroys them after a profiler's
+    // exit handler, which crashed under rocprofv3 in round 1).
+    // MPX_POOL_EXIT=keep leaves them to the runtime; MPX_POOL_EXIT_DELAY_MS
+    // sets the wait (A/B knobs).
+    const char* mode = getenv("MPX_POOL_EXIT");
+    if (mode && !strcmp(mode, "keep")) return;
+    const char* delay = getenv("MPX_POOL_EXIT_DELAY_MS");
+    const int delay_ms = (delay && *delay) ? atoi(delay) : 50;
+    if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] exit: destroying %zu pooled rank streams\n", p.all.size());
     int prev = -1;
     (void)hipGetDevice(&prev);
     for (auto& ds : p.all) {
         (void)hipSetDevice(ds.first);
         (void)hipStreamSynchronize(ds.second);
+    }
+    if (delay_ms > 0) usleep((useconds_t)delay_ms * 1000u);
+    for (auto& ds : p.all) {
+        (void)hipSetDevice(ds.first);
         (void)hipStreamDestroy(ds.second);
     }
     if (prev >= 0) (void)hipSetDevice(prev);
     p.all.clear();
     p.idle.clear();
+    if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] exit: rank streams destroyed\n");
 }
 
 bool same_device(const Rank& a, const Rank& b) {

@@ -39,7 +39,9 @@
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
 #endif
+#include <dirent.h>
 #include <errno.h>
+#include <execinfo.h>
 #include <pthread.h>
 #include <signal.h>
 #include <stdint.h>
@@ -47,6 +49,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -397,9 +400,48 @@ static void connect_ranks(void)
         if (q != me && strcmp(host_of[q], host_of[me]) == 0) MPX_CHECK(mpx_rank_import(ctx, q, all[q]));
 }
 
+/* Diagnostics (MPX_DEBUG set): `kill -USR1 <pid>` prints the stack of every
+   thread of the process to stderr, so a run that stalls — inside a loop, a
+   teardown or the runtime's exit — says where. */
+static void dump_this_thread(int sig)
+{
+    (void)sig;
+    void *pc[48];
+    char hdr[64];
+    const int n = snprintf(hdr, sizeof hdr, "[mpx] thread %ld:\n", (long)syscall(SYS_gettid));
+    if (write(2, hdr, (size_t)n) < 0) return;
+    backtrace_symbols_fd(pc, backtrace(pc, 48), 2);
+}
+
+static void dump_all_threads(int sig)
+{
+    const long self = (long)syscall(SYS_gettid);
+    DIR *d = opendir("/proc/self/task");
+    if (d) {
+        struct dirent *e;
+        while ((e = readdir(d)) != NULL) {
+            const long tid = atol(e->d_name);
+            if (tid <= 0 || tid == self) continue;
+            syscall(SYS_tgkill, (long)getpid(), tid, SIGUSR2);
+            usleep(20000);   /* one stack at a time */
+        }
+        closedir(d);
+    }
+    dump_this_thread(sig);
+}
+
+static void install_stack_dump(void)
+{
+    void *warm[2];
+    (void)backtrace(warm, 2);   /* loads the unwinder now, not inside a handler */
+    signal(SIGUSR2, dump_this_thread);
+    signal(SIGUSR1, dump_all_threads);
+}
+
 int main(int argc, char **argv)
 {
     int lrank = 0, lsize = 1;
+    if (getenv("MPX_DEBUG")) install_stack_dump();
     const char *launch = getenv("MPX_LAUNCH");
     const int found = mpxb_launcher(&lrank, &lsize, &local_rank);
     procs = found && lsize > 1 && !(launch && !strcmp(launch, "threads"));

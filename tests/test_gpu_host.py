@@ -8,6 +8,8 @@ import subprocess
 
 import pytest
 
+from proc import run_bounded
+
 import oracle_py as O
 
 pytestmark = pytest.mark.gpu
@@ -24,7 +26,7 @@ def run(tmp_path, args, lines=("vm",), names="vm,runsc", gpus="0,0"):
     # MPX_HOSTNAME=localhost: the ranks' host IPv4 is 127.0.0.1, as in the
     # golden runs, so whole record lines compare (mpi_perf.c:236-237,551-554)
     env = dict(os.environ, MPX_PROCESSOR_NAMES=names, MPX_HOSTNAME="localhost")
-    p = subprocess.run([PERF, "-g", gpus, "-t", "5000"] + argv, capture_output=True, text=True, env=env, timeout=120)
+    p = run_bounded([PERF, "-g", gpus, "-t", "5000"] + argv, env=env)
     recs = []
     for f in sorted(glob.glob(str(logs / "tcp-*.log"))):
         recs += [line.rstrip("\n").split(",") for line in open(f)]
@@ -143,9 +145,8 @@ def test_log_rotation_and_ingest_hook(tmp_path):
     g1.write_text("vm\n")
     env = dict(os.environ, MPX_PROCESSOR_NAMES="vm,runsc", MPX_LOG_REFRESH_SEC="0.001", MPX_INGEST_CMD=env_cmd,
                MPX_HOSTNAME="localhost")
-    p = subprocess.run([PERF, "-g", "0,0", "-w", "2", "-f", str(g1), "-n", "1", "-p", "1", "-u", "1", "-r", "6",
-                        "-i", "20000", "-b", "8", "-l", str(tmp_path / "logs")], capture_output=True, text=True,
-                       env=env, timeout=120)
+    p = run_bounded([PERF, "-g", "0,0", "-w", "2", "-f", str(g1), "-n", "1", "-p", "1", "-u", "1", "-r", "6",
+                        "-i", "20000", "-b", "8", "-l", str(tmp_path / "logs")], env=env)
     assert p.returncode == 0, p.stderr[-600:]
     opened = hook.read_text().count("ingest") if hook.exists() else 0
     files = list((tmp_path / "logs").glob("tcp-*.log"))
@@ -274,8 +275,8 @@ def test_windows_front_end_runs_and_records(tmp_path, engine):
     g1.write_text("10.0.0.2\n")
     logs = tmp_path / "logs"
     env = dict(os.environ, MPX_PROCESSOR_NAMES="10.0.0.1,10.0.0.2")
-    p = subprocess.run([win, str(g1), "1", "1", "20", "65541", "4", str(logs), "-g", "0,0", "-e", engine,
-                        "-c", "1", "-t", "5000"], capture_output=True, text=True, env=env, timeout=120)
+    p = run_bounded([win, str(g1), "1", "1", "20", "65541", "4", str(logs), "-g", "0,0", "-e", engine,
+                     "-c", "1", "-t", "5000"], env=env)
     assert p.returncode == 0, p.stderr[-600:]
     assert len(re.findall(r"^INFO: ", p.stdout, re.M)) == 2 and "UUID:" not in p.stderr
     assert re.search(r"\[Run#: 0\]: Total time: ", p.stderr)

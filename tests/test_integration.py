@@ -23,6 +23,8 @@ import subprocess
 
 import pytest
 
+from proc import run_bounded
+
 import oracle_py as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,7 +39,7 @@ needs_bin = pytest.mark.skipif(not (os.path.exists(BIN) and os.path.exists(MPIEX
                                reason="patched reference not built (needs /root/reference: make -C oracle ref-mpx)")
 
 
-def launch(tmp_path, case, env_extra=None, timeout=120):
+def launch(tmp_path, case, env_extra=None, timeout=90):
     """The golden case's launch (tests/golden/gen_golden.py), with the patched
     binary.  Host names localhost / 127.0.0.1 resolve anywhere, so the record
     IPs are 127.0.0.1 as in the golden runs."""
@@ -54,7 +56,7 @@ def launch(tmp_path, case, env_extra=None, timeout=120):
     for k, v in (env_extra or {}).items():
         cmd += ["-genv", k, v]
     cmd += [WRAP, BIN] + argv
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=tmp_path)
+    p = run_bounded(cmd, timeout=timeout, env=env, cwd=tmp_path)
     recs = []
     for f in sorted(glob.glob(str(logs / "tcp-*.log"))):
         recs += [line.rstrip("\n").split(",") for line in open(f)]

@@ -9,9 +9,10 @@ payload checked, records in the log folder."""
 import glob
 import os
 import re
-import subprocess
 
 import pytest
+
+from proc import run_bounded
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PAIR = os.path.join(ROOT, "scripts", "run-gpu-pair.sh")
@@ -20,11 +21,11 @@ INFO = re.compile(r"INFO: (\S+), rank (\d+) out of (\d+) ranks, my_group: (\d), 
                   r"group_rank: (\d+), my_peer: (-?\d+)")
 
 
-def run(script, tmp_path, env, *args, timeout=120):
-    e = dict(os.environ, MPX_PROCESSOR_NAMES="", MPX_HOSTNAME="node", LOGFOLDER=str(tmp_path / "logs"))
+def run(script, tmp_path, env, *args, timeout=90):
+    # MPX_DEBUG: libmpx traces its teardown, so a run that stalls at exit says so
+    e = dict(os.environ, MPX_PROCESSOR_NAMES="", MPX_HOSTNAME="node", LOGFOLDER=str(tmp_path / "logs"), MPX_DEBUG="1")
     e.update(env)
-    return subprocess.run(["bash", script, *args], capture_output=True, text=True, env=e, timeout=timeout,
-                          cwd=tmp_path)
+    return run_bounded(["bash", script, *args], timeout=timeout, env=e, cwd=tmp_path)
 
 
 def records(tmp_path):
