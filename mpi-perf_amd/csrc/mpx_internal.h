@@ -146,11 +146,11 @@ hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int*
 // all `iters` copies in one launch with a grid barrier between steps; *bar
 // must be 0 at launch
 constexpr int kCopyStepsMaxGrid = 1024;   // 4 workgroups per CU: always co-resident
-// copies up to 2 MiB run as k_copy_steps: faster than a launch per copy
-// there (2 MiB 2.60 vs 3.20 us), even at 4 MiB (2.95 vs 3.18 us, but 3.80 in
-// a later bench run) and slower from 8 MiB (3.66 vs 3.31 us;
-// profiles/r02_copy_steps_variants.jsonl)
-constexpr size_t kCopyStepsDefaultMax = (size_t)2 << 20;
+// copies up to 1 MiB run as k_copy_steps: faster than a launch per copy
+// there (1 MiB 2.0-2.7 vs 3.0-3.2 us); from 2 MiB a launch per copy is as fast
+// or faster (2 MiB 2.52 vs 2.78-3.01 us, 16 MiB 4.22 vs 5.15-5.95;
+// profiles/r02_copy_steps_upl.jsonl, r02_copy_steps_mid.jsonl)
+constexpr size_t kCopyStepsDefaultMax = (size_t)1 << 20;
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
                              int* grid_out);
 hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s);

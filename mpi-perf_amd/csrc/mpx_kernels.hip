@@ -930,13 +930,12 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
     // profiles/r02_copy_steps_variants.jsonl); no store drain before arrival
     // (the barrier orders issue, not acknowledgement: -0.05..0.1 us per step);
     // the grid sized for `upl` 16-B units per lane per step, all of a lane's
-    // loads in flight at once: 1 up to 128 KiB, 4 at 256-512 KiB, 8 at
-    // 1 MiB, 2 above (profiles/r02_copy_steps_upl.jsonl: 512 KiB 2.14 ->
+    // loads in flight at once: 1 up to 128 KiB, 4 at 256-512 KiB, 8 above (profiles/r02_copy_steps_upl.jsonl: 512 KiB 2.14 ->
     // 1.82 us, 1 MiB 2.20 -> 2.02 against one unit per lane; below 256 KiB
     // the two bench sweeps disagreed by more than the A/B's difference).
     // MPX_COPY_STEPS="grid_cap:xcd:drain:upl" overrides (A/B knobs, read per call).
     int cap = 64, xcd = 0, drain = 0;
-    int upl = n <= ((size_t)128 << 10) ? 1 : n <= ((size_t)512 << 10) ? 4 : n <= ((size_t)1 << 20) ? 8 : 2;
+    int upl = n <= ((size_t)128 << 10) ? 1 : n <= ((size_t)512 << 10) ? 4 : 8;
     if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d:%d", &cap, &xcd, &drain, &upl);
     if (cap < 1 || cap > kCopyStepsMaxGrid) cap = kCopyStepsMaxGrid;
     if (upl < 1) upl = 1;

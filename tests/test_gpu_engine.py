@@ -42,24 +42,32 @@ def test_fill_and_checksum_match_oracle(ctx, n, pattern):
         ctx.free(b)
 
 
-@pytest.mark.parametrize("iters", [1, 7])
-@pytest.mark.parametrize("n", [1, 4096 + 5, (1 << 20) + 3, (2 << 20), (2 << 20) + 16, (8 << 20) + 1])
+@pytest.mark.parametrize("iters", [1, 2, 7])
+@pytest.mark.parametrize("n", [1, 4096 + 5, (128 << 10) + 1, (512 << 10) + 7, (1 << 20), (1 << 20) + 3, (2 << 20) + 16,
+                               (8 << 20) + 1])
 def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
-    """k_copy_steps (all copies in one launch, grid barrier between steps) at
-    the grid-size classes of its defaults (one workgroup; <= 64 with one
-    counter; 256 with the per-XCD counters) and both sides of the 2 MiB
-    threshold, plus every A/B knob combination at 1 MiB: output against the
+    """k_copy_steps (all copies in one launch, grid barrier between steps),
+    forced at every size (MPX_COPY_STEPS_MAX): the grid classes of its
+    defaults (one workgroup; <= 64 workgroups with 1, 4 or 8 units per lane
+    and per-lane load batches) on both sides of each class boundary and of
+    the 1 MiB default threshold, plus the A/B knob combinations (grid cap,
+    per-XCD counters, drain, units per lane) at 1 MiB + 3: output against the
     oracle's pattern, nothing written past the end."""
+    monkeypatch.setenv("MPX_COPY_STEPS_MAX", str(16 << 20))
     key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
     try:
         ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
-        variants = [None] + (["64:0:1", "256:1:1", "1024:1:0", "1:0:0"] if n == (1 << 20) + 3 else [])
+        variants = [None] + (["64:0:1:1", "256:1:1:8", "1024:1:0:2", "1:0:0:1", "64:0:0:8", "16:0:0:3"]
+                             if n == (1 << 20) + 3 else [])
         for v in variants:
             if v:
                 monkeypatch.setenv("MPX_COPY_STEPS", v)
             ctx.fill(dst, n + 64, mpx.FILL_BYTE, 0xEE)
             t = ctx.copy(0, dst, src, n, iters)
+            # one copy is one plain k_copy launch; more run as k_copy_steps
+            assert t.launches == 1 and mpx.PROTOCOLS.get(t.protocol) == ("copy_steps" if iters > 1 else "copy"), \
+                (v, t.protocol)
             assert ctx.checksum(dst, n) == O.pattern_checksum(n, mpx.FILL_SPLITMIX, key), v
             assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
             assert t.bytes == n * iters
@@ -80,8 +88,8 @@ def test_copy_kernel_matches_oracle(ctx, n):
         # nothing written past the end
         assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
         assert t.bytes == 2 * n
-        # both copies in one k_copy_steps launch up to 2 MiB, a launch each above
-        steps = 0 < n <= (2 << 20)
+        # both copies in one k_copy_steps launch up to 1 MiB, a launch each above
+        steps = 0 < n <= (1 << 20)
         assert t.launches == (1 if steps else 2 if n else 0)
         if n:
             assert mpx.PROTOCOLS[t.protocol] == ("copy_steps" if steps else "copy")
