@@ -114,7 +114,8 @@ def test_loops_reach_libmpx_without_gpu(tmp_path):
 
 GPU_CASES = ["pingpong_p1_b1_i10", "pingpong_p1_b456131_i3", "unidir_p1_b8_i10", "unidir_p1_b456131_i3",
              "nonblocking_p1_b4096_i7", "nonblocking_window_i600", "pingpong_p2_b4096_i7", "unidir_p2_b456131_i3",
-             "zero_bytes_pingpong"]
+             "zero_bytes_pingpong", "zero_iters", "unidir_wins_over_nonblocking", "summary_every_1000",
+             "max_int_buffer"]
 
 
 @pytest.mark.gpu
@@ -137,6 +138,9 @@ def test_patched_reference_receives_match_reference(tmp_path, case, engine):
         ref = c["shim"][str(r)]
         assert (d["recv_done"], d["recv_bytes"], d["recv_digest"]) == \
             (ref["recv_done"], ref["recv_bytes"], ref["recv_digest"]), (r, d, ref)
+    # the reference's run summary every 1000 runs (mpi_perf.c:564-568)
+    assert sorted(int(m) for m in re.findall(r"^\[Run#: (\d+)\]: Total time", p.stderr, flags=re.M)) == \
+        c["summaries"]
     # records: the reference's own writer (mpi_perf.c:551-554); everything
     # but time / uuid / timestamp compares, first 8 by (rank, run id) as kept
     recs.sort(key=lambda f: (int(f[2]), int(f[10])))
