@@ -16,7 +16,7 @@
 #define MPXH_DEF_BUF_SZ 456131     /* DEF_BUF_SZ             mpi_perf.c:14  */
 #define MPXH_DEF_ITERS 10          /* DEF_ITERS              mpi_perf.c:15  */
 #define MPXH_LOG_REFRESH_SEC 900   /* LOG_REFRESH_TIME_SEC   mpi_perf.c:16  */
-#define MPXH_MAX_RANKS 16
+#define MPXH_MAX_RANKS 64
 
 /* struct options, mpi_perf.c:257-268, plus the MI355X-only settings.  The
    first nine fields keep the reference's meaning and defaults. */

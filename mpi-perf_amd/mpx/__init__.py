@@ -28,9 +28,9 @@ MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
 MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": MODE_UNIDIR}
 FILL_BYTE, FILL_SPLITMIX = 0, 1
 XFER_STREAM = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 PATTERN_SEED = 0x6D70695F70657266
-MAX_RANKS = 16
+MAX_RANKS = 64
 RANK_DESC_BYTES = 512
 RCCL_ID_BYTES = 128
 PROTOCOLS = {0: "ll", 1: "bulk", 2: "sdma", 3: "rccl", 4: "copy", 5: "copy_steps"}

@@ -28,7 +28,7 @@ def test_every_header_symbol_is_exported():
 
 def test_version_and_strerror():
     L = mpx.lib()
-    assert L.mpx_version() == 2   # mpx_timing gained recv_done / recv_digest
+    assert L.mpx_version() == 3   # 2: mpx_timing gained recv_done / recv_digest; 3: 64 ranks per context
     texts = {L.mpx_strerror(i).decode() for i in range(9)}
     assert len(texts) == 9
     assert L.mpx_strerror(12345) == b"unknown mpx status"
@@ -49,7 +49,7 @@ def test_argument_validation_without_gpu():
 
 def test_header_constants_match_binding():
     txt = open(mpx.HEADER_PATH).read()
-    assert "#define MPX_MAX_RANKS 16" in txt and mpx.MAX_RANKS == 16
+    assert "#define MPX_MAX_RANKS 64" in txt and mpx.MAX_RANKS == 64
     assert "#define MPX_RANK_DESC_BYTES 512" in txt
     assert "0x6d70695f70657266ULL" in txt and mpx.PATTERN_SEED == 0x6D70695F70657266
     assert "#define MPX_LINK_XGMI 4" in txt and mpx.LINK_TYPES[4] == "xgmi"

@@ -225,3 +225,39 @@ def test_same_node_pairs_pass_the_node_check(tmp_path):
                           extra_env={"MPX_PROCESSOR_NAMES": "nodeA-0,nodeA-1"})
     assert "different hosts" not in "".join(errs)
     assert "hipGetDeviceCount" in "".join(errs)
+
+
+REF = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
+WRAP = os.path.join(ROOT, "oracle", "ref_wrap.sh")
+
+
+@pytest.mark.skipif(not (os.path.exists(REF) and os.path.exists(MPIEXEC)),
+                    reason="compiled reference not built (make -C oracle ref)")
+@pytest.mark.parametrize("flows", [8, 10])
+def test_hbv3_shape_pairing_matches_the_live_reference(tmp_path, flows):
+    """run-hbv3.sh's launch shape, 2 hosts x `flows` ranks (scripts/run-hbv3.sh:
+    -np 20 --map-by ppr:10:node, -p 10): beyond the golden fixtures' ppn <= 4,
+    so the compiled reference runs here, live, as the checker (-d 1: no
+    transfer).  mpx_perf -w 2*flows must print the same pairing (mpi_perf.c:
+    437-461) and the same number of launcher lines (:147-168)."""
+    n = 2 * flows
+    (tmp_path / "group1").write_text("vm\n")
+    args = ["-f", "group1", "-n", "1", "-p", str(flows), "-u", "1", "-d", "1", "-r", "2", "-i", "10", "-b", "456131",
+            "-l", "logs"]
+    (tmp_path / "logs").mkdir()
+    ref = subprocess.run([MPIEXEC, "-np", str(n), "-genv", "PPN", str(flows), "-genv", "HOST1", "vm", "-genv", "HOST0",
+                          "runsc", WRAP, REF] + args, capture_output=True, text=True, cwd=tmp_path, timeout=120)
+    assert ref.returncode == 0, ref.stderr[-600:]
+    names = ",".join(["vm"] * flows + ["runsc"] * flows)
+    ours = subprocess.run([PERF, "-w", str(n)] + args, capture_output=True, text=True, cwd=tmp_path, timeout=60,
+                          env=dict(os.environ, MPX_PROCESSOR_NAMES=names, MPX_HOSTNAME="localhost"))
+    assert ours.returncode == 0, ours.stderr[-600:]
+
+    def pairing(err):
+        return sorted((int(x[1]), int(x[2]), int(x[3]), int(x[4]), int(x[5]), int(x[6])) for x in INFO.findall(err))
+
+    want = pairing(ref.stderr)
+    assert len(want) == n and all(r[5] == (r[0] + flows) % n for r in want)
+    assert pairing(ours.stderr) == want
+    count = lambda err: len(re.findall(r"^dotnet ", err, flags=re.M))  # noqa: E731
+    assert count(ours.stderr) == count(ref.stderr) == 2 * n
