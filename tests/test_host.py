@@ -245,3 +245,41 @@ def test_kusto_file_selection_on_a_directory_mpx_perf_wrote(tmp_path):
         assert [os.path.basename(f) for f in picked] == \
             sorted(tcp, key=lambda f: os.path.getmtime(logs / f))[:-n]
         assert not any(os.path.basename(f).startswith("gpu-") for f in picked)
+
+
+# ---- properties over random layouts (hypothesis) ---------------------------
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.integers(0, 1), min_size=1, max_size=64))
+def test_pairing_matches_oracle_for_any_group_layout(H, groups):
+    """Any group assignment of up to 64 ranks (MPX_MAX_RANKS): the C rule
+    (mpxh_pairing), its Python mirror and the oracle's restatement of
+    mpi_perf.c:225-233,447-450 agree on group rank and peer, including ranks
+    left without a peer (-1)."""
+    n = len(groups)
+    g = (C.c_int * n)(*groups)
+    gr, gs, pe = (C.c_int * n)(), (C.c_int * n)(), (C.c_int * n)()
+    H.mpxh_pairing(n, g, gr, gs, pe)
+    assert pairing_from_groups(groups) == (list(gr), list(pe))
+    assert O.pairing(groups) == (list(gr), list(pe))
+    assert list(gs) == [groups.count(x) for x in groups]
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.integers(1, 32).map(lambda k: 2 * k))
+def test_rounds_are_perfect_matchings_covering_every_pair(H, n):
+    """Every even N up to 64: N-1 rounds, each a perfect matching, all
+    N(N-1)/2 pairs exactly once, and mpxh_round_role consistent with it."""
+    seen = set()
+    for r in range(n - 1):
+        pairs = (C.c_int * n)()
+        assert H.mpxh_round_pairs(n, r, pairs) == n // 2
+        ps = [(pairs[2 * k], pairs[2 * k + 1]) for k in range(n // 2)]
+        assert sorted(itertools.chain(*ps)) == list(range(n))
+        for a, b in ps:
+            seen.add((min(a, b), max(a, b)))
+            grp, peer = C.c_int(), C.c_int()
+            assert H.mpxh_round_role(n, r, b, C.byref(grp), C.byref(peer)) == 0 and (grp.value, peer.value) == (0, a)
+    assert len(seen) == n * (n - 1) // 2
