@@ -1145,6 +1145,75 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     return MPX_OK;
 }
 
+namespace {
+
+// A local rank's own resources: mailbox, stream, events, status, scratch,
+// checksum arrays and the check-mode receive ring (rk.dev current).
+int attach_resources(Rank& rk) {
+    HIPCK(hipDeviceGetPCIBusId(rk.bus_id, sizeof rk.bus_id, rk.dev));
+    TRY(alloc_mailbox(rk));
+    TRY(create_rank_stream(rk.dev, &rk.stream));
+    HIPCK(hipMemsetAsync(rk.mb, 0, sizeof(Mailbox), rk.stream));
+    HIPCK(hipEventCreate(&rk.ev0));
+    HIPCK(hipEventCreate(&rk.ev1));
+    HIPCK(hipHostMalloc(reinterpret_cast<void**>(&rk.status), sizeof(Status), hipHostMallocCoherent | hipHostMallocMapped));
+    memset(rk.status, 0, sizeof(Status));
+    HIPCK(hipMalloc(&rk.scratch, kScratchWords * sizeof(u64)));
+    HIPCK(hipMemsetAsync(rk.scratch, 0, kScratchWords * sizeof(u64), rk.stream));
+    TRY(ensure_csum(rk, 1024));
+    // receive slots of non-blocking check mode (IPC-exportable like rx)
+    rk.ring_bytes = ring_bytes_for(rk.len);
+    if (rk.ring_bytes) {
+        void* p = nullptr;
+        const hipError_t e = hipMalloc(&p, rk.ring_bytes);
+        if (e == hipErrorOutOfMemory) return fail(MPX_ERR_NOMEM, "check ring of %llu B on device %d",
+                                                  (unsigned long long)rk.ring_bytes, rk.dev);
+        HIPCK(e);
+        rk.ring = static_cast<unsigned char*>(p);
+    }
+    HIPCK(hipStreamSynchronize(rk.stream));
+    return MPX_OK;
+}
+
+// Frees what attach_resources allocated, on a failed attach: the stream is
+// drained first and goes back to the pool (the teardown rule above
+// create_rank_stream: free, never destroy).
+void release_rank(Rank& rk) {
+    if (rk.stream) (void)hipStreamSynchronize(rk.stream);
+    if (rk.mb) (void)hipFree(rk.mb);
+    if (rk.ring) (void)hipFree(rk.ring);
+    if (rk.scratch) (void)hipFree(rk.scratch);
+    if (rk.csum) (void)hipFree(rk.csum);
+    for (void* q : rk.retired) (void)hipFree(q);
+    if (rk.status) (void)hipHostFree(rk.status);
+    if (rk.ev0) (void)hipEventDestroy(rk.ev0);
+    if (rk.ev1) (void)hipEventDestroy(rk.ev1);
+    if (rk.stream) release_rank_stream(rk.dev, rk.stream);
+    (void)hipGetLastError();
+    rk = Rank{};
+}
+
+// Peer access between `dev` and the GPU of every local rank (ctx->mu held).
+int enable_peer_access(mpx_ctx* ctx, int dev) {
+    for (int i = 0; i < MPX_MAX_RANKS; ++i) {
+        const Rank& o = ctx->r[i];
+        if (!o.local || o.dev == dev) continue;
+        int can = 0;
+        HIPCK(hipDeviceCanAccessPeer(&can, dev, o.dev));
+        if (!can) return fail(MPX_ERR_UNSUPPORTED, "GPU %d cannot access GPU %d (no xGMI/P2P path)", dev, o.dev);
+        for (int dir = 0; dir < 2; ++dir) {
+            const int a = dir ? o.dev : dev, b = dir ? dev : o.dev;
+            DeviceGuard ga(a);
+            const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCK(e);
+            (void)hipGetLastError();
+        }
+    }
+    return MPX_OK;
+}
+
+}  // namespace
+
 int mpx_rank_attach(mpx_ctx* ctx, int rank, int dev, void* tx, void* rx, size_t len) {
     if (!ctx) return fail(MPX_ERR_INVALID, "ctx is NULL");
     if (rank < 0 || rank >= ctx->nranks) return fail(MPX_ERR_INVALID, "rank %d not in [0,%d)", rank, ctx->nranks);
@@ -1169,44 +1238,12 @@ int mpx_rank_attach(mpx_ctx* ctx, int rank, int dev, void* tx, void* rx, size_t 
     rk.tx = static_cast<unsigned char*>(tx);
     rk.rx = static_cast<unsigned char*>(rx);
     rk.len = len;
-    HIPCK(hipDeviceGetPCIBusId(rk.bus_id, sizeof rk.bus_id, dev));
-    TRY(alloc_mailbox(rk));
-    TRY(create_rank_stream(dev, &rk.stream));
-    HIPCK(hipMemsetAsync(rk.mb, 0, sizeof(Mailbox), rk.stream));
-    HIPCK(hipEventCreate(&rk.ev0));
-    HIPCK(hipEventCreate(&rk.ev1));
-    HIPCK(hipHostMalloc(reinterpret_cast<void**>(&rk.status), sizeof(Status), hipHostMallocCoherent | hipHostMallocMapped));
-    memset(rk.status, 0, sizeof(Status));
-    HIPCK(hipMalloc(&rk.scratch, kScratchWords * sizeof(u64)));
-    HIPCK(hipMemsetAsync(rk.scratch, 0, kScratchWords * sizeof(u64), rk.stream));
-    TRY(ensure_csum(rk, 1024));
-    // receive slots of non-blocking check mode (IPC-exportable like rx)
-    rk.ring_bytes = ring_bytes_for(len);
-    if (rk.ring_bytes) {
-        void* p = nullptr;
-        const hipError_t e = hipMalloc(&p, rk.ring_bytes);
-        if (e == hipErrorOutOfMemory) return fail(MPX_ERR_NOMEM, "check ring of %llu B on device %d",
-                                                  (unsigned long long)rk.ring_bytes, dev);
-        HIPCK(e);
-        rk.ring = static_cast<unsigned char*>(p);
-    }
-    HIPCK(hipStreamSynchronize(rk.stream));
-
+    int st = attach_resources(rk);
     std::lock_guard<std::mutex> lk(ctx->mu);
-    // peer access between this rank's GPU and every other local rank's GPU
-    for (int i = 0; i < MPX_MAX_RANKS; ++i) {
-        const Rank& o = ctx->r[i];
-        if (!o.local || o.dev == dev) continue;
-        int can = 0;
-        HIPCK(hipDeviceCanAccessPeer(&can, dev, o.dev));
-        if (!can) return fail(MPX_ERR_UNSUPPORTED, "GPU %d cannot access GPU %d (no xGMI/P2P path)", dev, o.dev);
-        for (int dir = 0; dir < 2; ++dir) {
-            const int a = dir ? o.dev : dev, b = dir ? dev : o.dev;
-            DeviceGuard ga(a);
-            const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCK(e);
-            (void)hipGetLastError();
-        }
+    if (st == MPX_OK) st = enable_peer_access(ctx, dev);
+    if (st != MPX_OK) {
+        release_rank(rk);   // nothing of a failed attach stays allocated
+        return st;
     }
     if (ctx->import_dev < 0) ctx->import_dev = dev;
     ctx->r[rank] = rk;
