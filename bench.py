@@ -590,12 +590,13 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
 
 
 def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                        extras: dict) -> tuple[dict, str]:
+                        extras: dict, latency: bool = True) -> tuple[dict, str]:
     """pairs_bench on `engine`; if the kernel engine fails (payload
     validation, or a device timeout on any rank in validation or in the timed
     steps), measure the SDMA engine instead and say so: an explicit, labelled
     fallback, never a silent one."""
-    res = pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync)
+    res = pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
+                      latency=latency)
     engine_used = engine
     if res.get("error") and engine == "kernel":
         extras["kernel_engine_error"] = res["error"]
@@ -603,7 +604,7 @@ def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iter
         # own buffers, so it is the last resort when IPC itself failed
         for fb_engine in ("sdma", "rccl"):
             fb = pairs_bench(mpx, torch, dist, fb_engine, rank, world, dev, nbytes, iters, steps, warmup,
-                             barrier_sync)
+                             barrier_sync, latency=latency)
             if not fb.get("error"):
                 res, engine_used = fb, f"{fb_engine} (fallback: kernel engine failed, extras.kernel_engine_error)"
                 break
@@ -740,8 +741,11 @@ def main() -> None:
     else:
         workload = "all_pairs_rounds_unidir"
         metric_unit = "GB/s"
+        # --no-extras: nothing after the timed steps (profiling runs select
+        # the timed launches as the last ones)
         res, engine_used = pairs_with_fallback(mpx, torch, dist, args.engine, rank, world, dev, nbytes, iters,
-                                               args.steps, args.warmup, barrier_sync, extras)
+                                               args.steps, args.warmup, barrier_sync, extras,
+                                               latency=not args.no_extras)
         elapsed, total = res["elapsed"], res["total"]
         achieved = res["per_pair_GBps"]
         roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",

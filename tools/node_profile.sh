@@ -1,0 +1,47 @@
+#!/bin/bash
+# Counters of the N-GPU bench path ("rocprof counters (achieved
+# xGMI and HBM GB/s) ... at 2, 4 and 8 GPUs").  Every rank of bench.py is
+# started by hand (no launcher hop under the profiler), each under its own
+# rocprofv3:
+#   pass 1  --kernel-trace --stats            k_xfer durations per rank
+#   pass 2  --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum
+#           (three of the four TCC counters one pass may hold); a sender's
+#           link traffic is (WRREQ - WRREQ_DRAM) x 64 B per dispatch
+# then tools/node_profile_summary.py writes gpurun_out/node_prof_n$N/summary.json.
+#
+#   N=8 tools/node_profile.sh                 on an 8-GPU node (one rank per GPU)
+#   N=2 MPX_BENCH_ONE_GPU=1 tools/node_profile.sh   rehearsal on one GPU: only
+#       rank 0 is counter-profiled (the GPU's counters are shared), and every
+#       write lands in local DRAM, so the link traffic reads 0
+# Each rank has its own time limit; the script fails if any rank fails.
+set -o pipefail
+N=${N:-2}
+O=gpurun_out/node_prof_n$N
+mkdir -p $O
+export TMPDIR=/tmp WORLD_SIZE=$N MASTER_ADDR=127.0.0.1
+STEPS=${STEPS:-$((2 * (N - 1)))}
+run_pass() {   # pass-name, rocprofv3 options...
+    local pass=$1; shift
+    export MASTER_PORT=$((29600 + RANDOM % 300))
+    local pids=() r
+    for r in $(seq 0 $((N - 1))); do
+        local prof=("$@")
+        if [ -n "$MPX_BENCH_ONE_GPU" ] && [ "$pass" = pmc ] && [ $r -gt 0 ]; then prof=(); fi
+        if [ ${#prof[@]} -gt 0 ]; then
+            RANK=$r LOCAL_RANK=$r timeout -k 10 300 rocprofv3 "${prof[@]}" --output-format csv -d $O/$pass -o rank$r \
+                -- python3 -u bench.py --gpus $N --steps $STEPS --warmup 1 --no-extras \
+                > $O/${pass}_rank$r.json 2> $O/${pass}_rank$r.err &
+        else
+            RANK=$r LOCAL_RANK=$r timeout -k 10 300 python3 -u bench.py --gpus $N --steps $STEPS --warmup 1 --no-extras \
+                > $O/${pass}_rank$r.json 2> $O/${pass}_rank$r.err &
+        fi
+        pids+=($!)
+    done
+    local rc=0 p
+    for p in "${pids[@]}"; do wait $p || rc=1; done
+    echo "node_profile N=$N pass $pass rc=$rc"
+    return $rc
+}
+run_pass trace --kernel-trace --stats &&
+run_pass pmc --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum &&
+python3 tools/node_profile_summary.py $O $N
