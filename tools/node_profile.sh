@@ -7,6 +7,8 @@
 #   pass 2  --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum
 #           (three of the four TCC counters one pass may hold); a sender's
 #           link traffic is (WRREQ - WRREQ_DRAM) x 64 B per dispatch
+#   pass 3  --pmc TCC_EA0_WRREQ_WRITE_GMI_32B_sum TCC_EA0_WRREQ_WRITE_IO_32B_sum:
+#           which fabric path the non-DRAM writes take (32-B units)
 # then tools/node_profile_summary.py writes gpurun_out/node_prof_n$N/summary.json.
 #
 #   N=8 tools/node_profile.sh                 on an 8-GPU node (one rank per GPU)
@@ -26,7 +28,7 @@ run_pass() {   # pass-name, rocprofv3 options...
     local pids=() r
     for r in $(seq 0 $((N - 1))); do
         local prof=("$@")
-        if [ -n "$MPX_BENCH_ONE_GPU" ] && [ "$pass" = pmc ] && [ $r -gt 0 ]; then prof=(); fi
+        if [ -n "$MPX_BENCH_ONE_GPU" ] && [ "$pass" != trace ] && [ $r -gt 0 ]; then prof=(); fi
         if [ ${#prof[@]} -gt 0 ]; then
             RANK=$r LOCAL_RANK=$r timeout -k 10 300 rocprofv3 "${prof[@]}" --output-format csv -d $O/$pass -o rank$r \
                 -- python3 -u bench.py --gpus $N --steps $STEPS --warmup 1 --no-extras \
@@ -44,4 +46,5 @@ run_pass() {   # pass-name, rocprofv3 options...
 }
 run_pass trace --kernel-trace --stats &&
 run_pass pmc --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum &&
+run_pass fabric --pmc TCC_EA0_WRREQ_WRITE_GMI_32B_sum TCC_EA0_WRREQ_WRITE_IO_32B_sum &&
 python3 tools/node_profile_summary.py $O $N

@@ -67,6 +67,18 @@ def main():
                 rec["link_over_algorithmic"] = round((wr - dram) * 64 / (B * iters), 4)
                 if "avg_launch_us" in rec:
                     rec["achieved_link_GBps"] = round((wr - dram) * 64 / (rec["avg_launch_us"] * 1e-6) / 1e9, 2)
+        fb = glob.glob(os.path.join(out_dir, "fabric", f"rank{r}_counter_collection.csv"))
+        if fb and k:
+            per = {}
+            for x in csv.DictReader(open(fb[0])):
+                if SENDER in x["Kernel_Name"]:
+                    per.setdefault(int(x["Dispatch_Id"]), {})[x["Counter_Name"]] = float(x["Counter_Value"])
+            last = [per[i] for i in sorted(per)[-k:]]
+            if last:
+                rec["gmi_write_bytes_per_launch"] = round(
+                    statistics.median(v.get("TCC_EA0_WRREQ_WRITE_GMI_32B_sum", 0) for v in last) * 32)
+                rec["io_write_bytes_per_launch"] = round(
+                    statistics.median(v.get("TCC_EA0_WRREQ_WRITE_IO_32B_sum", 0) for v in last) * 32)
         ranks.append(rec)
     doc = dict(n=n, bytes=B, iters_per_step=iters, steps=steps, kernel=SENDER,
                source="tools/node_profile.sh: rocprofv3 --kernel-trace --stats, then --pmc TCC_EA0_WRREQ_sum "
