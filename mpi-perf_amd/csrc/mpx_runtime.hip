@@ -570,6 +570,26 @@ int stream_check(Rank& me, long long n, int i, int iters, unsigned char* buf = n
     return MPX_OK;
 }
 
+// The SDMA engine's payload copy kind.  Between two GPUs it is
+// hipMemcpyDeviceToDeviceNoCU: the runtime must use a copy engine (SDMA), the
+// engine north_star (b) names.  Within one GPU (loopback pairs) it is the
+// plain device-to-device kind, which the runtime runs as its blit kernel on
+// the CUs (profiles/r02_sdma_engine_loopback_kernel_stats.csv): two ranks of
+// one GPU share its SDMA queues, and a copy waiting at the head of a shared
+// queue for its own rank's poll blocks the other rank's copy behind it — the
+// loopback ping-pong timed out that way with NoCU copies
+// (profiles/r02_sdma_kind_ab.jsonl), which also moved 40 GB/s against the
+// blit kernel's 570 on one GPU.  A rank paired with itself has one stream and
+// cannot deadlock so.  MPX_SDMA_KIND=nocu|blit forces one kind (A/B).
+hipMemcpyKind sdma_kind(bool same_gpu) {
+    static const int forced = [] {
+        const char* v = getenv("MPX_SDMA_KIND");
+        return !v ? 0 : !strcmp(v, "nocu") ? 1 : !strcmp(v, "blit") ? 2 : 0;
+    }();
+    const bool nocu = forced == 1 || (forced == 0 && !same_gpu);
+    return nocu ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
+}
+
 // non-blocking publish schedule shared by the kernel and SDMA engines: every
 // nb_publish() pushes, at window slot 254 (the last receive a Waitall(255)
 // waits for, so no flush waits for the slot-255 push the reference leaves
@@ -594,7 +614,8 @@ struct SdmaOps {
     // time out.
     int push(long long n, u64 seq, bool publish = true, bool skip_copy = false) {
         if (n > 0 && !skip_copy) {
-            HIPCK(hipMemcpyAsync(peer.rx, me.tx, (size_t)n, hipMemcpyDeviceToDevice, me.stream));
+            HIPCK(hipMemcpyAsync(peer.rx, me.tx, (size_t)n, sdma_kind(&me != &peer && same_device(me, peer)),
+                                 me.stream));
             ++launches;
         }
         if (!publish) return MPX_OK;
@@ -661,7 +682,7 @@ struct SdmaOps {
             TRY(wait_abs(credit_in, tx0 + (u64)(i >= slots ? i - slots + 1 : 0)));
             if (len > 0 && skip != i + 1) {
                 HIPCK(hipMemcpyAsync(slot_ptr(peer, i, iters, slots, len), me.tx, (size_t)len,
-                                     hipMemcpyDeviceToDevice, me.stream));
+                                     sdma_kind(same_device(me, peer) && &me != &peer), me.stream));
                 ++launches;
             }
             TRY(signal_abs(&peer.mb->flag[my_slot][0], tx0 + i + 1));
