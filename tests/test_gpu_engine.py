@@ -318,6 +318,25 @@ def test_timeout_when_peer_never_runs():
         P.close()
 
 
+@pytest.mark.parametrize("check", [True, False])
+@pytest.mark.parametrize("mode", [mpx.MODE_PINGPONG, mpx.MODE_NONBLOCKING])
+def test_sdma_engine_drains_fast_when_the_peer_never_runs(mode, check):
+    """The SDMA engine enqueues a bounded wait per receive (hundreds per call).
+    Once one of them times out, every later wait of the call returns at once,
+    so the call ends in about one deadline, not one per remaining wait (an
+    exited peer used to hold the stream, and the process exit, for minutes)."""
+    import time
+    P = Pairs("sdma", 1, 65536)
+    try:
+        t0 = time.monotonic()
+        out, errs = P.run(mode, 4096, 600, timeout_ms=200, ranks=[0], check=check)
+        took = time.monotonic() - t0
+        assert 0 in errs and errs[0].status == mpx.ERR_TIMEOUT, errs
+        assert took < 10, took     # 600 waits x 200 ms would be 120 s
+    finally:
+        P.close()
+
+
 def test_check_mode_detects_missing_payload():
     """Tell the receiver to expect a different payload: every iteration fails."""
     P = Pairs("kernel", 1, 65536)
