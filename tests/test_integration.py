@@ -18,8 +18,10 @@ completed, bytes and digest are compared with the reference's own ranks
 import glob
 import json
 import os
+import pathlib
 import re
 import subprocess
+import tempfile
 
 import pytest
 
@@ -147,3 +149,52 @@ def test_patched_reference_receives_match_reference(tmp_path, case, engine):
     assert len(recs) == c["n_records"]
     assert [",".join(["T", "U"] + f[2:9] + ["X"] + f[10:]) for f in recs[:8]] == \
         [x["line_masked"] for x in c["records"]]
+
+
+# ---- random configurations against the live reference (GPU box) -----------
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
+
+
+def _shim_json(prefix, np_):
+    return [json.load(open(f"{prefix}.{r}.json")) for r in range(np_)]
+
+
+@pytest.mark.gpu
+@needs_bin
+@pytest.mark.skipif(not os.path.exists(REF), reason="compiled reference not built")
+@settings(max_examples=30, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(mode=st.sampled_from(["pingpong", "nonblocking", "unidir"]), ppn=st.sampled_from([1, 2]),
+       B=st.one_of(st.integers(0, 64), st.integers(65, 300000)), iters=st.integers(1, 40),
+       window=st.booleans(), engine=st.sampled_from(["kernel", "sdma"]))
+def test_random_runs_match_the_live_reference(tmp_path, mode, ppn, B, iters, window, engine):
+    """A random (loop, ppn, B, iterations) — beyond the golden fixtures — run
+    twice: by the compiled reference itself on the host (MPICH shared memory,
+    the PMPI shim digesting every receive it completes) and by the same
+    reference main() over libmpx on GPU 0 (every payload checksummed on the
+    device).  Per rank: receives completed, bytes and digest must be equal.
+    The non-blocking loop sometimes runs 255-600 iterations (its window)."""
+    if mode == "nonblocking" and window:
+        iters = 255 + iters * 9          # 264 .. 615: one or two flushes, slot 255 left pending
+    np_ = 2 * ppn
+    d = pathlib.Path(tempfile.mkdtemp(dir=tmp_path))
+    (d / "group1").write_text("localhost\n")
+    (d / "logs").mkdir()
+    args = ["-f", "group1", "-n", "1", "-p", str(ppn), "-r", "2", "-i", str(iters), "-b", str(B), "-l", "logs"]
+    args += {"pingpong": [], "nonblocking": ["-x", "1"], "unidir": ["-u", "1"]}[mode]
+    base = [MPIEXEC, "-np", str(np_), "-genv", "PPN", str(ppn), "-genv", "HOST1", "localhost", "-genv", "HOST0",
+            "127.0.0.1"]
+    shim = str(d / "shim")
+    ref = run_bounded(base + ["-genv", "SHIM_OUT", shim, WRAP, REF] + args, timeout=60, cwd=d,
+                      env=dict(os.environ, SHIM_OUT=shim))
+    assert ref.returncode == 0, ref.stderr[-800:]
+    out = str(d / "recv")
+    env = {"MPX_CHECK": "1", "MPX_RECV_OUT": out, "MPX_ENGINE": engine}
+    ours = run_bounded(base + sum((["-genv", k, v] for k, v in env.items()), []) + [WRAP, BIN] + args, timeout=60,
+                       cwd=d, env=dict(os.environ, **env))
+    assert ours.returncode == 0, ours.stderr[-800:]
+    want = [(x["recv_done"], x["recv_bytes"], x["recv_digest"]) for x in _shim_json(shim, np_)]
+    got = [(x["recv_done"], x["recv_bytes"], x["recv_digest"]) for x in _shim_json(out, np_)]
+    assert got == want, (mode, ppn, B, iters, engine)
