@@ -3,8 +3,10 @@ records, log files and check mode, compared with the reference's golden
 runs (same flags) and the record format."""
 import glob
 import os
+import pathlib
 import re
 import subprocess
+import tempfile
 
 import pytest
 
@@ -294,3 +296,50 @@ def test_windows_front_end_runs_and_records(tmp_path, engine):
     assert len(side) == 3
     for f in side:
         assert f[4] == "2" and int(f[15]) == 20 and int(f[16]) == 0   # unidir, 20 checked, 0 failures
+
+
+# ---- random runs against the live reference --------------------------------
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
+WRAP = os.path.join(ROOT, "oracle", "ref_wrap.sh")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+
+@pytest.mark.skipif(not (os.path.exists(REF) and os.path.exists(MPIEXEC)), reason="compiled reference not built")
+@settings(max_examples=20, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(mode=st.sampled_from([[], ["-x", "1"], ["-u", "1"], ["-u", "1", "-x", "1"]]), ppn=st.sampled_from([1, 2]),
+       B=st.one_of(st.integers(0, 64), st.integers(65, 300000)), iters=st.integers(1, 30), runs=st.integers(0, 4),
+       engine=st.sampled_from(["kernel", "sdma"]))
+def test_random_runs_records_match_the_live_reference(tmp_path, mode, ppn, B, iters, runs, engine):
+    """mpx_perf (GPU 0, every payload checked) and the compiled reference
+    (host, MPICH shm) with the same random flags: the same record lines
+    (timestamp, job id and time masked; mpi_perf.c:545-555 — only group 1,
+    only runs 1..), the same INFO pairing, and every payload passed."""
+    np_ = 2 * ppn
+    d = pathlib.Path(tempfile.mkdtemp(dir=tmp_path))
+    (d / "group1").write_text("localhost\n")
+    args = ["-f", str(d / "group1"), "-n", "1", "-p", str(ppn), "-r", str(runs), "-i", str(iters), "-b", str(B)] + mode
+    (d / "ref_logs").mkdir()
+    ref = run_bounded([MPIEXEC, "-np", str(np_), "-genv", "PPN", str(ppn), "-genv", "HOST1", "localhost", "-genv",
+                       "HOST0", "127.0.0.1", WRAP, REF] + args + ["-l", str(d / "ref_logs")], timeout=60, cwd=d)
+    assert ref.returncode == 0, ref.stderr[-600:]
+    want = []
+    for f in sorted(glob.glob(str(d / "ref_logs" / "tcp-*.log"))):
+        want += [mask_record(line.rstrip("\n").split(",")) for line in open(f)]
+    names = ",".join(["localhost"] * ppn + ["127.0.0.1"] * ppn)
+    env = dict(os.environ, MPX_PROCESSOR_NAMES=names, MPX_HOSTNAME="localhost")
+    ours = run_bounded([PERF, "-w", str(np_), "-g", ",".join(["0"] * np_), "-e", engine, "-t", "5000", "-c", "1"] + args
+                       + ["-l", str(d / "logs")], env=env, cwd=d)
+    assert ours.returncode == 0, ours.stderr[-600:]
+    got, side = [], []
+    for f in sorted(glob.glob(str(d / "logs" / "tcp-*.log"))):
+        got += [mask_record(line.rstrip("\n").split(",")) for line in open(f)]
+    for f in sorted(glob.glob(str(d / "logs" / "gpu-*.csv"))):
+        side += [line.rstrip("\n").split(",") for line in open(f)][1:]
+    assert sorted(got) == sorted(want), (args, engine)
+    assert all(int(f[16]) == 0 and int(f[15]) == iters for f in side), side[:2]
+    info = lambda e: sorted(re.findall(r"INFO: \S+, rank (\d+) out of (\d+) ranks, my_group: (\d), "  # noqa: E731
+                                       r"group_size: (\d+), group_rank: (\d+), my_peer: (-?\d+)", e))
+    assert info(ours.stderr) == info(ref.stderr)
