@@ -49,4 +49,4 @@ with mpx.Context(2, "sdma") as c:
                 t.append(max(out[0].device_s, out[1].device_s) / iters * 1e6)
         us = statistics.median(t)
         res[name] = dict(us_per_iter=round(us, 3), GBps=round(n / us / 1e3, 2))
-    print(json.dumps(dict(kind=os.environ.get("MPX_SDMA_KIND", "nocu"), results=res)), flush=True)
+    print(json.dumps(dict(kind=os.environ.get("MPX_SDMA_KIND", "auto"), results=res)), flush=True)
