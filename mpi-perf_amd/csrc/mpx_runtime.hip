@@ -310,9 +310,11 @@ bool plain_streams() {
 // ("a0 m0 k0.0 d0 f0" hangs at exit; "a0 m0 k0.0 f0 d0" is fine; freeing a
 // buffer no kernel touched is fine either way).  Even with every allocation
 // of a context freed before its streams are destroyed, a long-lived process
-// that creates and finalizes contexts one after another hung in a later
-// context's first hipMalloc/launch (the -m gpu suite, ~60 contexts in:
-// profiles/r02_stream_destroy_suite_hang.txt).  So rank streams are
+// that creates and finalizes contexts one after another stalled in a later
+// context (the -m gpu suite: profiles/r02_stream_destroy_suite_hang.txt,
+// r02_stream_pool_ab.txt) unless the destroy waits ~50 ms after the drain —
+// the runtime still finishes a drained stream's last commands on its HSA
+// event thread (the exit stall below, same race).  So rank streams are
 // process-lifetime objects, like the runtime's own queues: mpx_finalize
 // drains them, frees every allocation of the context, and returns them to a
 // per-device pool that later contexts reuse; an exit handler destroys the
@@ -338,7 +340,35 @@ StreamPool& pool() {
 void destroy_stream_pool();
 
 void release_rank_stream(int dev, hipStream_t s) {
+    // MPX_STREAM_POOL=0: every mpx_finalize destroys its rank streams,
+    // MPX_STREAM_POOL_DELAY_MS (default 50) after their drain — the same
+    // wait as at exit (destroy_stream_pool).  With it the engine tests pass
+    // with a destroy per finalize; without it they stalled inside a later
+    // mpx_finalize (profiles/r02_stream_pool_ab.txt).  Opt-in: the pool never
+    // destroys a stream while the process runs.
+    static const bool no_pool = [] {
+        const char* v = getenv("MPX_STREAM_POOL");
+        return v && atoi(v) == 0;
+    }();
+    static const int delay_ms = [] {
+        const char* v = getenv("MPX_STREAM_POOL_DELAY_MS");
+        return v ? atoi(v) : 50;
+    }();
     if (plain_streams()) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    if (no_pool) {
+        {
+            std::lock_guard<std::mutex> lk(pool().mu);
+            auto& all = pool().all;
+            for (size_t i = 0; i < all.size(); ++i)
+                if (all[i].second == s) {
+                    all.erase(all.begin() + (long)i);
+                    break;
+                }
+        }
+        if (delay_ms > 0) usleep((useconds_t)delay_ms * 1000u);
         (void)hipStreamDestroy(s);
         return;
     }
