@@ -160,7 +160,9 @@ int mpx_finalize(mpx_ctx *ctx);
 
 /* ---- buffers (allocate_tx_rx_buffers, mpi_perf.c:240-252) ---------------- */
 /* posix_memalign(4096) analogue: device memory on `dev`, 4 KiB aligned.  The
-   allocation is exportable to other processes (IPC) and peer-mappable. */
+   allocation is exportable to other processes (IPC) and peer-mappable.
+   bytes == 0 yields a zeroed 16-byte block: the unidir ack still reads
+   tx[0] at -b 0 (mpi_perf.c:142), which is 0 in the reference. */
 int mpx_alloc(mpx_ctx *ctx, int dev, size_t bytes, void **ptr);
 /* free() analogue (mpi_perf.c:576-577) */
 int mpx_free(mpx_ctx *ctx, void *ptr);

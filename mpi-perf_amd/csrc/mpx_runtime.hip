@@ -1088,6 +1088,17 @@ int mpx_alloc(mpx_ctx* ctx, int dev, size_t bytes, void** ptr) {
         (void)hipFree(p);
         return fail(MPX_ERR_HIP, "hipMalloc returned a pointer that is not 4 KiB aligned");
     }
+    // -b 0: the unidir ack still sends tx[0] (mpi_perf.c:142) out of a 0-byte
+    // posix_memalign block — glibc hands back a fresh zeroed chunk, so the
+    // reference's ack byte is 0 (its PMPI digest, tests/test_integration.py);
+    // the 16-byte pad is zeroed to match
+    if (!bytes) {
+        const hipError_t z = hipMemset(p, 0, 16);
+        if (z != hipSuccess) {
+            (void)hipFree(p);
+            HIPCK(z);
+        }
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->allocs[reinterpret_cast<uintptr_t>(p)] = AllocRec{dev, bytes};
     *ptr = p;

@@ -277,8 +277,10 @@ int oracle_run_pairs(int npairs, int mode, int iters, size_t B, oracle_rank_stat
         const size_t cap = B ? B : 1;
         if (posix_memalign((void **)&j.ep[r].tx, 4096, cap) || posix_memalign((void **)&j.ep[r].rx, 4096, cap))
             return -1;
-        /* allocate_tx_rx_buffers, mpi_perf.c:244-251: group 0 'a', group 1 'b' */
-        memset(j.ep[r].tx, r < npairs ? 'b' : 'a', cap);
+        /* allocate_tx_rx_buffers, mpi_perf.c:244-251: group 0 'a', group 1 'b'.
+           At B = 0 the memset writes nothing, yet the unidir ack still sends
+           tx[0] (:142): a fresh glibc chunk's 0 (golden zero_bytes_unidir) */
+        memset(j.ep[r].tx, B ? (r < npairs ? 'b' : 'a') : 0, cap);
         memset(j.ep[r].rx, 0, cap);
         atomic_init(&j.ep[r].arrived, 0);
         memset(&stats[r], 0, sizeof stats[r]);

@@ -121,6 +121,11 @@ def main():
                                                     "-l", "@LOGS"]))
     cases.append(run_case("zero_bytes_pingpong", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-r", "2", "-i", "5",
                                                         "-b", "0", "-l", "@LOGS"]))
+    # the ack is tx[0:1) even at -b 0 (mpi_perf.c:142): a byte of a 0-byte block
+    cases.append(run_case("zero_bytes_unidir", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-r", "2", "-i", "5",
+                                                      "-b", "0", "-l", "@LOGS", "-u", "1"]))
+    cases.append(run_case("zero_bytes_nonblocking", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-r", "2", "-i", "5",
+                                                           "-b", "0", "-l", "@LOGS", "-x", "1"]))
     # --- group rule: case-insensitive prefix over the processor name ---
     cases.append(run_case("group_upper_prefix_line", 2, 1, ["-f", "@G1", "-n", "1", "-p", "1", "-r", "2", "-i", "3",
                                                             "-b", "8", "-l", "@LOGS"], group1_lines=("VMX",)))

@@ -8,7 +8,7 @@ names.  Every combination carries -d 1, so neither side moves data
 exit status (0, 255 for MPI_Abort, SIGFPE for the reference's division by a
 zero ppn), the error message, every rank's INFO pairing (mpi_perf.c:460), the
 launcher lines (:147-168) and the rank-0 summaries (:564-568).  Beyond the
-61 golden fixtures, this covers the option parser, defaults and validation
+63 golden fixtures, this covers the option parser, defaults and validation
 (:257-339, :388-403) on inputs nobody wrote down.
 """
 import os

@@ -307,7 +307,8 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
 
 
 @pytest.mark.skipif(not (os.path.exists(REF) and os.path.exists(MPIEXEC)), reason="compiled reference not built")
-@settings(max_examples=20, deadline=None, derandomize=True,
+@settings(max_examples=int(os.environ.get("MPX_FUZZ_EXAMPLES", "20")), deadline=None,
+          derandomize=not os.environ.get("MPX_FUZZ_EXAMPLES"),
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 @given(mode=st.sampled_from([[], ["-x", "1"], ["-u", "1"], ["-u", "1", "-x", "1"]]), ppn=st.sampled_from([1, 2]),
        B=st.one_of(st.integers(0, 64), st.integers(65, 300000)), iters=st.integers(1, 30), runs=st.integers(0, 4),

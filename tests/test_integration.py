@@ -116,8 +116,8 @@ def test_loops_reach_libmpx_without_gpu(tmp_path):
 
 GPU_CASES = ["pingpong_p1_b1_i10", "pingpong_p1_b456131_i3", "unidir_p1_b8_i10", "unidir_p1_b456131_i3",
              "nonblocking_p1_b4096_i7", "nonblocking_window_i600", "pingpong_p2_b4096_i7", "unidir_p2_b456131_i3",
-             "zero_bytes_pingpong", "zero_iters", "unidir_wins_over_nonblocking", "summary_every_1000",
-             "max_int_buffer"]
+             "zero_bytes_pingpong", "zero_bytes_unidir", "zero_bytes_nonblocking", "zero_iters",
+             "unidir_wins_over_nonblocking", "summary_every_1000", "max_int_buffer"]
 
 
 @pytest.mark.gpu
@@ -164,7 +164,8 @@ def _shim_json(prefix, np_):
 @pytest.mark.gpu
 @needs_bin
 @pytest.mark.skipif(not os.path.exists(REF), reason="compiled reference not built")
-@settings(max_examples=30, deadline=None, derandomize=True,
+@settings(max_examples=int(os.environ.get("MPX_FUZZ_EXAMPLES", "30")), deadline=None,
+          derandomize=not os.environ.get("MPX_FUZZ_EXAMPLES"),
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 @given(mode=st.sampled_from(["pingpong", "nonblocking", "unidir"]), ppn=st.sampled_from([1, 2]),
        B=st.one_of(st.integers(0, 64), st.integers(65, 300000)), iters=st.integers(1, 40),

@@ -61,7 +61,8 @@ def test_strnicmp_prefix_semantics():
 
 
 LOOP_CASES = [c["name"] for c in G["cases"] if re.match(r"(pingpong|nonblocking|unidir)_p\d_b\d+_i\d+$", c["name"])]
-LOOP_CASES += ["defaults_unidir", "zero_bytes_pingpong", "group_upper_prefix_line"]
+LOOP_CASES += ["defaults_unidir", "zero_bytes_pingpong", "zero_bytes_unidir", "zero_bytes_nonblocking",
+               "group_upper_prefix_line"]
 
 
 @pytest.mark.parametrize("name", LOOP_CASES)
