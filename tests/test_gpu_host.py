@@ -301,6 +301,10 @@ def test_windows_front_end_runs_and_records(tmp_path, engine):
 # ---- random runs against the live reference --------------------------------
 from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
 
+# the LL/bulk protocol switch (2 KiB on one GPU, 8 KiB across GPUs: ll_max_bytes,
+# csrc/mpx_internal.h) and 16-B unit tails on either side of it
+LL_EDGES = [15, 16, 17, 2047, 2048, 2049, 4096, 8191, 8192, 8193, 16383, 16384, 16385]
+
 REF = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
 WRAP = os.path.join(ROOT, "oracle", "ref_wrap.sh")
 MPIEXEC = "/opt/conda/bin/mpiexec"
@@ -311,7 +315,8 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
           derandomize=not os.environ.get("MPX_FUZZ_EXAMPLES"),
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 @given(mode=st.sampled_from([[], ["-x", "1"], ["-u", "1"], ["-u", "1", "-x", "1"]]), ppn=st.sampled_from([1, 2]),
-       B=st.one_of(st.integers(0, 64), st.integers(65, 300000)), iters=st.integers(1, 30), runs=st.integers(0, 4),
+       B=st.one_of(st.integers(0, 64), st.sampled_from(LL_EDGES), st.integers(65, 300000)),
+       iters=st.integers(1, 30), runs=st.integers(0, 4),
        engine=st.sampled_from(["kernel", "sdma"]))
 def test_random_runs_records_match_the_live_reference(tmp_path, mode, ppn, B, iters, runs, engine):
     """mpx_perf (GPU 0, every payload checked) and the compiled reference

@@ -154,6 +154,10 @@ def test_patched_reference_receives_match_reference(tmp_path, case, engine):
 # ---- random configurations against the live reference (GPU box) -----------
 from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
 
+# the LL/bulk protocol switch (2 KiB on one GPU, 8 KiB across GPUs: ll_max_bytes,
+# csrc/mpx_internal.h) and 16-B unit tails on either side of it
+LL_EDGES = [15, 16, 17, 2047, 2048, 2049, 4096, 8191, 8192, 8193, 16383, 16384, 16385]
+
 REF = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
 
 
@@ -168,7 +172,7 @@ def _shim_json(prefix, np_):
           derandomize=not os.environ.get("MPX_FUZZ_EXAMPLES"),
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 @given(mode=st.sampled_from(["pingpong", "nonblocking", "unidir"]), ppn=st.sampled_from([1, 2]),
-       B=st.one_of(st.integers(0, 64), st.integers(65, 300000)), iters=st.integers(1, 40),
+       B=st.one_of(st.integers(0, 64), st.sampled_from(LL_EDGES), st.integers(65, 300000)), iters=st.integers(1, 40),
        window=st.booleans(), engine=st.sampled_from(["kernel", "sdma"]))
 def test_random_runs_match_the_live_reference(tmp_path, mode, ppn, B, iters, window, engine):
     """A random (loop, ppn, B, iterations) — beyond the golden fixtures — run
