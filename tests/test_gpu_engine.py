@@ -213,7 +213,7 @@ def test_receive_digest_matches_reference(name, engine):
     iters = int(a[a.index("-i") + 1]) if "-i" in a else 10
     B = int(a[a.index("-b") + 1]) if "-b" in a else 456131
     mode = mpx.MODE_UNIDIR if "-u" in a else (mpx.MODE_NONBLOCKING if "-x" in a else mpx.MODE_PINGPONG)
-    P = Pairs(engine, ppn, max(B, 1))
+    P = Pairs(engine, ppn, B)   # B = 0: mpx_alloc's zeroed pad, whose byte 0 the unidir ack sends (mpi_perf.c:142)
     try:
         digest = {r: [0, 0, 0] for r in range(2 * ppn)}
         for _ in range(runs):

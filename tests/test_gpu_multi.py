@@ -121,7 +121,7 @@ def test_cfg3_receive_digest_matches_reference_across_gpus(name, engine):
     iters = int(a[a.index("-i") + 1]) if "-i" in a else 10
     B = int(a[a.index("-b") + 1]) if "-b" in a else 456131
     m = mpx.MODE_UNIDIR if "-u" in a else (mpx.MODE_NONBLOCKING if "-x" in a else mpx.MODE_PINGPONG)
-    P = Pairs(engine, ppn, max(B, 1), devs=cross_gpu_devs(2 * ppn))
+    P = Pairs(engine, ppn, B, devs=cross_gpu_devs(2 * ppn))
     try:
         digest = {r: [0, 0, 0] for r in range(2 * ppn)}
         for _ in range(runs):
