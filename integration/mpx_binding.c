@@ -62,6 +62,16 @@ static int g_dev, g_engine, g_check;
 static uint64_t *g_sum_len, *g_sum_one; /* per world rank: checksum of its tx[0:B), tx[0:1) */
 static unsigned long long g_recv_done, g_recv_bytes, g_recv_digest;
 
+static void *xmalloc(size_t n)
+{
+    void *p = malloc(n ? n : 1);
+    if (!p) {
+        fprintf(stderr, "[%s:%d] out of host memory (%zu bytes)\n", __FILE__, __LINE__, n);
+        exit(EXIT_FAILURE);
+    }
+    return p;
+}
+
 static int engine_from_env(void)
 {
     const char *e = getenv("MPX_ENGINE");
@@ -155,9 +165,9 @@ void allocate_tx_rx_buffers(void **buffer_tx, void **buffer_rx, int buff_len, in
     MPX_CHECK(mpx_checksum(g_mpx, g_dev, g_tx, len, &mine[0]));
     /* the ack is tx[0:1) even at -b 0 (mpi_perf.c:142; mpx_alloc zeroes the pad) */
     MPX_CHECK(mpx_checksum(g_mpx, g_dev, g_tx, 1, &mine[1]));
-    uint64_t *sums = malloc(sizeof(uint64_t) * 2 * (size_t)world_size);
-    g_sum_len = malloc(sizeof(uint64_t) * (size_t)world_size);
-    g_sum_one = malloc(sizeof(uint64_t) * (size_t)world_size);
+    uint64_t *sums = xmalloc(sizeof(uint64_t) * 2 * (size_t)world_size);
+    g_sum_len = xmalloc(sizeof(uint64_t) * (size_t)world_size);
+    g_sum_one = xmalloc(sizeof(uint64_t) * (size_t)world_size);
     MPI_Allgather(mine, 2, MPI_UINT64_T, sums, 2, MPI_UINT64_T, MPI_COMM_WORLD);
     for (int r = 0; r < world_size; ++r) {
         g_sum_len[r] = sums[2 * r];
@@ -181,8 +191,8 @@ void allocate_tx_rx_buffers(void **buffer_tx, void **buffer_rx, int buff_len, in
     gethostname(host, sizeof host - 1);
     unsigned char desc[MPX_RANK_DESC_BYTES];
     MPX_CHECK(mpx_rank_export(g_mpx, world_rank, desc));
-    unsigned char *all_desc = malloc((size_t)world_size * MPX_RANK_DESC_BYTES);
-    char *all_host = malloc((size_t)world_size * HOST_SZ);
+    unsigned char *all_desc = xmalloc((size_t)world_size * MPX_RANK_DESC_BYTES);
+    char *all_host = xmalloc((size_t)world_size * HOST_SZ);
     MPI_Allgather(desc, MPX_RANK_DESC_BYTES, MPI_BYTE, all_desc, MPX_RANK_DESC_BYTES, MPI_BYTE, MPI_COMM_WORLD);
     MPI_Allgather(host, HOST_SZ, MPI_CHAR, all_host, HOST_SZ, MPI_CHAR, MPI_COMM_WORLD);
     for (int r = 0; r < world_size; ++r)
