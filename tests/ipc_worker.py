@@ -22,7 +22,7 @@ def main():
     d, rank = sys.argv[1], int(sys.argv[2])
     engine = sys.argv[3] if len(sys.argv) > 3 else "kernel"
     # "cross": rank r on GPU r (the pair moves its bytes over xGMI); else GPU 0
-    dev = rank if len(sys.argv) > 4 and sys.argv[4] == "cross" else 0
+    dev = rank if len(sys.argv) > 4 and sys.argv[4] == "cross" and not os.environ.get("MPX_MULTI_REHEARSE") else 0
     peer = 1 - rank
     group = 1 if rank == 0 else 0
     cap = 1 << 20

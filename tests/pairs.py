@@ -12,13 +12,21 @@ rank on a GPU of its own, so each pair moves its bytes over xGMI.
 """
 from __future__ import annotations
 
+import os
 import threading
 
 import mpx
 
+# MPX_MULTI_REHEARSE=1: run the multi-GPU tests' code on one GPU (every rank
+# on GPU 0) to shake out the tests themselves; see tests/test_gpu_multi.py
+REHEARSE = bool(os.environ.get("MPX_MULTI_REHEARSE"))
+
 
 def cross_gpu_devs(nranks: int) -> list[int] | None:
-    """rank r on GPU r, or None when fewer than nranks GPUs are visible"""
+    """rank r on GPU r, or None when fewer than nranks GPUs are visible
+    (rehearsal: every rank on GPU 0)"""
+    if REHEARSE:
+        return [0] * nranks
     return list(range(nranks)) if mpx.device_count() >= nranks else None
 
 

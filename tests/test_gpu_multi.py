@@ -13,6 +13,13 @@ configuration each covers:
 
 Every payload is checksummed on the receiving device; receive accounting is
 compared with the compiled reference's golden runs where one exists.
+
+MPX_MULTI_REHEARSE=1 (with MPX_LL_MAX=8192, the cross-GPU LL threshold) runs
+this module on ONE GPU, every rank on GPU 0 and N = MPX_MULTI_REHEARSE_N
+(default 4) ranks where a test uses the whole node: it proves the tests'
+own code, not the links (tools/gpu_multi_rehearse.sh).  What only distinct
+GPUs have is skipped then: RCCL (it refuses two ranks on one GPU), the
+link table, and the "every pair spans two GPUs" check.
 """
 import glob
 import json
@@ -26,7 +33,7 @@ import pytest
 
 import mpx
 import oracle_py as O
-from pairs import Pairs, cross_gpu_devs
+from pairs import REHEARSE, Pairs, cross_gpu_devs
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -42,7 +49,12 @@ def ngpus() -> int:
     return mpx.device_count()
 
 
-def need(n: int):
+def need(n: int, engine: str = "", distinct: bool = False):
+    if REHEARSE:
+        if engine == "rccl" or distinct:
+            pytest.skip("needs distinct GPUs (one-GPU rehearsal)")
+        assert os.environ.get("MPX_LL_MAX") == "8192", "rehearse with the cross-GPU LL threshold: MPX_LL_MAX=8192"
+        return
     if ngpus() < n:
         pytest.skip(f"needs {n} GPUs, {ngpus()} visible")
 
@@ -58,7 +70,7 @@ def test_cfg3_cross_gpu_pair_every_payload(engine, mode):
     size around the cross-GPU LL threshold and up to 4 MiB, every payload
     checksummed on the receiver (reads of bytes the peer wrote over xGMI),
     receives counted on the device, final rx = the peer's tx."""
-    need(2)
+    need(2, engine)
     P = Pairs(engine, 1, 4 << 20, fill="seeded", devs=cross_gpu_devs(2))
     m = MODES[mode]
     try:
@@ -82,7 +94,7 @@ def test_cfg3_cross_gpu_pair_every_payload(engine, mode):
 def test_cfg3_cross_gpu_max_int_buffer(engine):
     """B = 2^31 - 1 (the reference's largest int buffer) across GPUs, every
     mode, every payload checked."""
-    need(2)
+    need(2, engine)
     P = Pairs(engine, 1, INT_MAX, fill="seeded", devs=cross_gpu_devs(2))
     try:
         for m in MODES.values():
@@ -115,7 +127,7 @@ def test_cfg3_receive_digest_matches_reference_across_gpus(name, engine):
     compiled reference's (PMPI shim) numbers."""
     c = GOLDEN[name]
     ppn = c["ppn"]
-    need(2 * ppn)
+    need(2 * ppn, engine)
     a = c["args"]
     runs = int(a[a.index("-r") + 1])
     iters = int(a[a.index("-i") + 1]) if "-i" in a else 10
@@ -143,7 +155,7 @@ def test_cfg3_receive_digest_matches_reference_across_gpus(name, engine):
 def test_cfg3_cross_gpu_two_processes_ipc(tmp_path, engine):
     """Two processes, rank r on GPU r, each mapping the other's rx, ring and
     mailbox through IPC (bench.py's one-process-per-GPU path)."""
-    need(2)
+    need(2, engine)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "ipc_worker.py"), str(tmp_path), str(r), engine,
                                "cross"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in (0, 1)]
     outs = []
@@ -194,6 +206,8 @@ def _files(tmp_path):
 
 
 def _world():
+    if REHEARSE:
+        return int(os.environ.get("MPX_MULTI_REHEARSE_N", "4"))
     n = ngpus()
     return n - (n & 1)
 
@@ -204,7 +218,7 @@ def test_cfg4_all_pairs_rounds_every_gpu(tmp_path, engine):
     4 concurrent pairs = all 28 pairs), unidir 456131 B x 10 (run-hbv3's
     shape), seeded payloads, every payload checked, records for runs 1..N-1
     covering every pair once."""
-    need(2)
+    need(2, engine)
     N = _world()
     (tmp_path / "group1").write_text("vm\n")
     names = ",".join(["vm"] * (N // 2) + ["runsc"] * (N // 2))
@@ -217,14 +231,15 @@ def test_cfg4_all_pairs_rounds_every_gpu(tmp_path, engine):
     assert {(int(f[2]), int(f[6])) for f in side} == {q for rnd in all_pairs_rounds(N) for q in rnd}
     assert len(recs) == (N - 1) * (N // 2)
     assert all(int(f[16]) == 0 and int(f[15]) == 10 and int(f[18]) == 10 for f in side)
-    assert all(f[5] != f[7] for f in side)                 # every pair spans two GPUs
+    if not REHEARSE:
+        assert all(f[5] != f[7] for f in side)             # every pair spans two GPUs
 
 
 def test_cfg5_rccl_all_pairs_stress_processes(tmp_path):
     """BASELINE config 5: one mpx_perf process per GPU (the reference's
     process model), RCCL engine, all-pairs rounds twice over, seeded payloads
     checked, and the records are what kusto_ingest.py would upload."""
-    need(2)
+    need(2, "rccl")
     N = _world()
     (tmp_path / "group1").write_text("vm\n")
     names = ",".join(["vm"] * (N // 2) + ["runsc"] * (N // 2))
@@ -256,7 +271,7 @@ def test_cfg5_rccl_all_pairs_stress_processes(tmp_path):
 
 def test_link_types_between_all_gpus():
     """Every pair of visible GPUs is one xGMI hop apart (full mesh)."""
-    need(2)
+    need(2, distinct=True)
     for a in range(ngpus()):
         for b in range(ngpus()):
             if a != b:
