@@ -7,8 +7,6 @@ through its C-ABI, checking every result against the oracle.
 import os
 import sys
 
-import pytest
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mpi-perf_amd")
 for p in (PKG, os.path.dirname(os.path.abspath(__file__))):
