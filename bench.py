@@ -21,7 +21,9 @@ A "step" is one run of the reference's loop (mpi_perf.c:474-569: barrier ->
   links.  After them come the per-pair table of every covered pair, a
   checked small-message ping-pong on every link, the 8 B latency (10^5
   ping-pong iterations on round 0, 10^4 on every pair), config 3's pair
-  sweep, run-hbv3's 456131 B x 10 rounds, and the SDMA and RCCL comparison
+  sweep, run-hbv3's 456131 B x 10 rounds, the same rounds at 64 MiB (the
+  link rate with the per-iteration protocol cost amortised away: the
+  reference point of the 4 MiB headline), and the SDMA and RCCL comparison
   engines under a watchdog.  A kernel-engine failure before or inside the
   timed steps falls back to SDMA (labelled); a failure after them nulls only
   its own numbers.
@@ -58,7 +60,8 @@ HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # roofline; the bidirectional figure is reported beside it.
 XGMI_LINK_PEAK_BIDIR_GBPS = 153.6
 XGMI_LINK_PEAK_GBPS = XGMI_LINK_PEAK_BIDIR_GBPS / 2
-EXTRAS_DEADLINE_S = 120      # comparison engines at N > 1 (see main)
+EXTRAS_DEADLINE_S = 150      # 64 MiB rounds + comparison engines at N > 1 (see main)
+CEILING_BYTES, CEILING_ITERS = 64 << 20, 20   # extras: the kernel engine at 64 MiB (see main)
 
 
 def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:
@@ -832,6 +835,19 @@ def main() -> None:
         dog = threading.Timer(EXTRAS_DEADLINE_S, on_deadline)
         dog.daemon = True
         dog.start()
+        if config["engine"] == "kernel":
+            # the same rounds at 64 MiB: the per-iteration protocol cost
+            # (drain, flag, 1-byte ack) is then ~0.5 % of a push, so this is
+            # the link rate the kernel engine reaches with B out of the
+            # picture, the reference point for the 4 MiB headline's fraction
+            r3 = pairs_bench(mpx, torch, dist, "kernel", rank, world, dev, CEILING_BYTES, CEILING_ITERS, world - 1, 1,
+                             barrier_sync, latency=False, tune=False)
+            if r3.get("error"):
+                extras["unidir_64MiB_per_pair_GBps"] = r3["error"]
+            else:
+                extras["unidir_64MiB_per_pair_GBps"] = round(r3["per_pair_GBps"], 2)
+                extras["unidir_64MiB_pair_GBps_min_max"] = r3.get("pair_GBps_min_max")
+                extras["headline_over_64MiB"] = round(achieved / r3["per_pair_GBps"], 4)
         for eng in ("sdma", "rccl"):
             if config["engine"].startswith(eng):
                 continue
