@@ -1091,11 +1091,20 @@ int mpx_alloc(mpx_ctx* ctx, int dev, size_t bytes, void** ptr) {
     // -b 0: the unidir ack still sends tx[0] (mpi_perf.c:142) out of a 0-byte
     // posix_memalign block — glibc hands back a fresh zeroed chunk, so the
     // reference's ack byte is 0 (its PMPI digest, tests/test_integration.py);
-    // the 16-byte pad is zeroed to match
+    // the 16-byte pad is zeroed to match, on the utility stream (the null
+    // stream would wait for other ranks' persistent kernels)
     if (!bytes) {
-        const hipError_t z = hipMemset(p, 0, 16);
-        if (z != hipSuccess) {
+        hipStream_t us = nullptr;
+        const int st = util_stream(ctx, dev, &us);
+        hipError_t z = hipSuccess;
+        if (st == MPX_OK) {
+            std::lock_guard<std::mutex> ul(ctx->util_mu);
+            z = hipMemsetAsync(p, 0, 16, us);
+            if (z == hipSuccess) z = hipStreamSynchronize(us);
+        }
+        if (st != MPX_OK || z != hipSuccess) {
             (void)hipFree(p);
+            if (st != MPX_OK) return st;
             HIPCK(z);
         }
     }
