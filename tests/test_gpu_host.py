@@ -315,7 +315,8 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
           derandomize=not os.environ.get("MPX_FUZZ_EXAMPLES"),
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 @given(mode=st.sampled_from([[], ["-x", "1"], ["-u", "1"], ["-u", "1", "-x", "1"]]), ppn=st.sampled_from([1, 2]),
-       B=st.one_of(st.integers(0, 64), st.sampled_from(LL_EDGES), st.integers(65, 300000)),
+       B=st.one_of(st.integers(0, 64), st.sampled_from(LL_EDGES), st.integers(65, 300000),
+                   st.integers(300001, 8 << 20)),
        iters=st.integers(1, 30), runs=st.integers(0, 4),
        engine=st.sampled_from(["kernel", "sdma"]))
 def test_random_runs_records_match_the_live_reference(tmp_path, mode, ppn, B, iters, runs, engine):

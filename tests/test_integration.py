@@ -172,7 +172,8 @@ def _shim_json(prefix, np_):
           derandomize=not os.environ.get("MPX_FUZZ_EXAMPLES"),
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 @given(mode=st.sampled_from(["pingpong", "nonblocking", "unidir"]), ppn=st.sampled_from([1, 2]),
-       B=st.one_of(st.integers(0, 64), st.sampled_from(LL_EDGES), st.integers(65, 300000)), iters=st.integers(1, 40),
+       B=st.one_of(st.integers(0, 64), st.sampled_from(LL_EDGES), st.integers(65, 300000),
+                   st.integers(300001, 8 << 20)), iters=st.integers(1, 40),
        window=st.booleans(), engine=st.sampled_from(["kernel", "sdma"]))
 def test_random_runs_match_the_live_reference(tmp_path, mode, ppn, B, iters, window, engine):
     """A random (loop, ppn, B, iterations) — beyond the golden fixtures — run
