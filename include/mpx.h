@@ -63,8 +63,13 @@ enum mpx_status {
 /* ---- transfer engines (north_star (a)/(b)/(c)) ------------------------- */
 enum mpx_engine {
     MPX_ENGINE_KERNEL = 0,    /* hand-written CDNA4 push kernels + device flags */
-    MPX_ENGINE_SDMA = 1,      /* hipMemcpyPeerAsync + stream wait/write value   */
-    MPX_ENGINE_RCCL = 2       /* ncclSend/ncclRecv                              */
+    MPX_ENGINE_SDMA = 1,      /* copy-engine hipMemcpyAsync (NoCU across GPUs)
+                                 + one-lane signal / bounded-wait kernels       */
+    MPX_ENGINE_RCCL = 2,      /* ncclSend/ncclRecv                              */
+    MPX_ENGINE_HOST = 3       /* SURVEY §8b's CPU engine: not built; mpx_init
+                                 returns MPX_ERR_UNSUPPORTED (the
+                                 CPU side is the compiled reference itself, and
+                                 libmpx has no CPU transfer path to fall into) */
 };
 
 /* ---- loop modes: the three reference loops ----------------------------- */

@@ -990,6 +990,9 @@ int mpx_init(int nranks, int engine, mpx_ctx** out) {
     if (!out) return fail(MPX_ERR_INVALID, "ctx out-pointer is NULL");
     *out = nullptr;
     if (nranks < 1 || nranks > MPX_MAX_RANKS) return fail(MPX_ERR_INVALID, "nranks %d not in [1,%d]", nranks, MPX_MAX_RANKS);
+    if (engine == MPX_ENGINE_HOST)
+        return fail(MPX_ERR_UNSUPPORTED, "engine HOST is not built: the CPU baseline is the compiled reference "
+                    "(DESIGN.md section 8)");
     if (engine < MPX_ENGINE_KERNEL || engine > MPX_ENGINE_RCCL) return fail(MPX_ERR_INVALID, "engine %d", engine);
     int ndev = 0;
     HIPCK(hipGetDeviceCount(&ndev));

@@ -23,6 +23,7 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "mpx.h")
 # enum values (include/mpx.h)
 OK, ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_TIMEOUT, ERR_RCCL, ERR_UNSUPPORTED, ERR_STATE, ERR_CHECK = range(9)
 ENGINE_KERNEL, ENGINE_SDMA, ENGINE_RCCL = 0, 1, 2
+ENGINE_HOST = 3   # reserved: mpx_init refuses it, MPX_ERR_UNSUPPORTED
 ENGINES = {"kernel": ENGINE_KERNEL, "sdma": ENGINE_SDMA, "rccl": ENGINE_RCCL}
 MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
 MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": MODE_UNIDIR}

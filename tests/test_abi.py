@@ -40,6 +40,9 @@ def test_argument_validation_without_gpu():
     assert L.mpx_init(0, 0, ctypes.byref(h)) == mpx.ERR_INVALID
     assert L.mpx_init(mpx.MAX_RANKS + 1, 0, ctypes.byref(h)) == mpx.ERR_INVALID
     assert L.mpx_init(2, 7, ctypes.byref(h)) == mpx.ERR_INVALID
+    # SURVEY §8b's HOST engine id is reserved and refused (no CPU transfer path)
+    assert L.mpx_init(2, mpx.ENGINE_HOST, ctypes.byref(h)) == mpx.ERR_UNSUPPORTED
+    assert b"HOST" in L.mpx_last_error()
     assert L.mpx_finalize(None) == mpx.ERR_INVALID
     assert L.mpx_xfer(None, 0, 1, 0, 1, 1, None, None, 8, None) == mpx.ERR_INVALID
     assert L.mpx_rccl_get_unique_id(None) == mpx.ERR_INVALID
