@@ -10,6 +10,8 @@ A "step" is one run of the reference's loop (mpi_perf.c:474-569: barrier ->
 * N = 1 — BASELINE config 2, the 1-GPU local device-to-device copy: each step
   is `iters` launches of the HBM copy kernel moving B = 1 GiB tx -> rx (the
   loop's degenerate pair, both ends on one GPU).  value = B*iters*K / T.
+  After the timed steps: config 2's sweep (1 B .. 1 GiB), the same copy held
+  for 6 s (sustained rate), loopback pair latency / rate, the runtime's copy.
 * N >= 2 — BASELINE config 4, all-pairs concurrent rounds (run-hbv3-style,
   unidirectional): step s runs round s mod (N-1) of the circle-method
   schedule; each of the N/2 pairs moves `iters` x 4 MiB G1 -> G0 over xGMI
@@ -148,6 +150,22 @@ def copy_sweep(mpx, c, src, dst, nbytes: int) -> dict:
            for k, (v, p) in sorted(best.items())}
     assert c.checksum(dst, b // 2) == c.checksum(src, b // 2), "copy sweep output differs from its input"
     return out
+
+
+def sustained_copy(c, src, dst, nbytes: int, seconds: float = 6.0) -> dict:
+    """The headline copy held for `seconds` of back-to-back launches (calls of
+    300 copies, ~0.1 s each at 1 GiB): whether the rate of the short timed
+    region holds once clocks and temperature settle.  HBM traffic (2B per
+    copy) per call from HIP events; the output is checked at the end."""
+    rates, t_end = [], time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        t = c.copy(0, dst, src, nbytes, 300)
+        rates.append(2 * nbytes * 300 / t.device_s / 1e9)
+    assert c.checksum(dst, nbytes) == c.checksum(src, nbytes), "sustained copy output differs from its input"
+    return dict(seconds=seconds, calls=len(rates), copies=300 * len(rates),
+                hbm_GBps_median=round(statistics.median(rates), 1), hbm_GBps_min=round(min(rates), 1),
+                hbm_GBps_max=round(max(rates), 1), hbm_GBps_last=round(rates[-1], 1),
+                frac_median=round(statistics.median(rates) / HBM_PEAK_GBPS, 4))
 
 
 def hbm_one_direction_ceiling() -> dict | None:
@@ -732,6 +750,7 @@ def main() -> None:
         metric_unit = "GB/s"
         if not args.no_extras:
             extras["copy_sweep"] = copy_sweep(mpx, c, src, dst, nbytes)
+            extras["sustained_copy"] = sustained_copy(c, src, dst, nbytes)
             lat = loopback_pair(mpx, "kernel", mpx.MODE_PINGPONG, 8, 5000)
             extras["loopback_pingpong_8B_half_rtt_us"] = round(lat["per_iter_us"] / 2, 3)
             uni = loopback_pair(mpx, "kernel", mpx.MODE_UNIDIR, 4 << 20, 200)
