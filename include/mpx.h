@@ -215,9 +215,12 @@ int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank
 
 /* Build, outside any timed region, what a later mpx_xfer_ex with the same
    (mode, group, ranks, iters, buff_len, opts) would otherwise build on its
-   first call: the SDMA engine's graph-captured loop chunks.  The reference's
-   timer brackets only the loop (mpi_perf.c:501-533), so hosts call this
-   before their barrier (mpi_perf.c:499).  A no-op for the other engines. */
+   first call: the SDMA engine's graph-captured loop chunks, or the RCCL
+   engine's p2p channel to peer_rank (a one-byte exchange, once per pair; both
+   ranks of the pair must call it, as they call the transfer).  The
+   reference's timer brackets only the loop (mpi_perf.c:501-533), so hosts
+   call this before their barrier (mpi_perf.c:499).  A no-op for the kernel
+   engine. */
 int mpx_xfer_prepare(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
                      int buff_len, const mpx_xfer_opts *opts);
 

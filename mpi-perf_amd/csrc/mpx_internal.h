@@ -59,7 +59,7 @@ struct Status {
 //   [0] grid-barrier counter  [1] abort word  [2] finished workgroups
 //   [4..5] SDMA engine's device-side sequence base {tx, rx}
 constexpr int kScratchWords = 8;
-constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrSeqBase = 4;
+constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrSeqBase = 4, kScrLink = 6;
 
 // Non-blocking check mode ("ring"): receive j of a call with `iters`
 // iterations lands in slot (iters-1-j) mod S of the receiver, where slot 0 is

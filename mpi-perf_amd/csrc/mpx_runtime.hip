@@ -117,6 +117,7 @@ struct Rank {
     u64 rx_seq[MPX_MAX_RANKS] = {};
     ncclComm_t comm = nullptr;
     int comm_rank = -1;
+    bool rccl_linked[MPX_MAX_RANKS] = {};          // RCCL p2p channel to that rank set up (mpx_xfer_prepare)
     std::map<SdmaKey, hipGraphExec_t> sdma_graphs;   // run_sdma's captured chunks
 };
 
@@ -1448,6 +1449,30 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     return MPX_OK;
 }
 
+namespace {
+// RCCL connects a pair lazily, on its first send/receive: transport setup and
+// the exchange of buffer handles, milliseconds across GPUs.  The reference's
+// MPI does the same, and its record of run 0 — the only run that pays it in a
+// reference job — is dropped (mpi_perf.c:545).  In all-pairs rounds every
+// round meets new peers, so runs 1..N-2 would carry that setup inside their
+// recorded time; a one-byte exchange here, once per pair, before the barrier,
+// takes it out.  Both ranks of the pair call it (as they call the transfer),
+// on the rank's stream, into scratch words no transfer uses.
+int rccl_link(Rank& me, int my_rank, int peer_rank) {
+    if (!me.comm) return fail(MPX_ERR_STATE, "rank %d has no RCCL communicator (mpx_rccl_init_*)", my_rank);
+    if (me.rccl_linked[peer_rank]) return MPX_OK;
+    DeviceGuard g(me.dev);
+    HIPCK(g.err);
+    NCCLCK(ncclGroupStart());
+    NCCLCK(ncclSend(me.scratch + kScrLink, 1, ncclChar, peer_rank, me.comm, me.stream));
+    NCCLCK(ncclRecv(me.scratch + kScrLink + 1, 1, ncclChar, peer_rank, me.comm, me.stream));
+    NCCLCK(ncclGroupEnd());
+    HIPCK(hipStreamSynchronize(me.stream));
+    me.rccl_linked[peer_rank] = true;
+    return MPX_OK;
+}
+}  // namespace
+
 int mpx_xfer_prepare(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, int buff_len,
                      const mpx_xfer_opts* opts) {
     if (!ctx) return fail(MPX_ERR_INVALID, "NULL argument");
@@ -1458,8 +1483,9 @@ int mpx_xfer_prepare(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer
     Rank& me = ctx->r[my_rank];
     Rank& peer = ctx->r[peer_rank];
     if (!me.local) return fail(MPX_ERR_STATE, "rank %d is not attached in this process", my_rank);
-    // only the SDMA engine builds anything per (mode, side, peer, B): the
-    // graph-captured chunks run_sdma replays (not used in check mode)
+    if (ctx->engine == MPX_ENGINE_RCCL) return rccl_link(me, my_rank, peer_rank);
+    // the SDMA engine builds its graph-captured chunks per (mode, side, peer,
+    // B): what run_sdma replays (not used in check mode)
     if (ctx->engine != MPX_ENGINE_SDMA || (opts && opts->check) || !sdma_graphs_enabled() || iters < kSdmaGraphMin)
         return MPX_OK;
     if (!peer.local && !peer.imported) return fail(MPX_ERR_STATE, "peer rank %d is unknown", peer_rank);

@@ -235,7 +235,8 @@ class Context:
 
     def prepare(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, length: int,
                 timeout_ms: int = 0) -> None:
-        """mpx_xfer_prepare: build the SDMA engine's graph chunks before timing"""
+        """mpx_xfer_prepare: before timing, build the SDMA engine's graph chunks or
+        set up the RCCL engine's channel to peer_rank (both ranks call it)"""
         o = XferOpts(timeout_ms=timeout_ms)
         check(self.L.mpx_xfer_prepare(self.h, mode, group, my_rank, peer_rank, iters, length, C.byref(o)),
               "mpx_xfer_prepare")

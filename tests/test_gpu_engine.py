@@ -499,6 +499,12 @@ def test_self_pair_nonblocking_every_payload(engine):
     cap = 456131
     c, tx, rx = _self_rank(engine, cap)
     try:
+        # mpx_xfer_prepare: SDMA graph chunks / the RCCL channel (a one-byte
+        # exchange, once per pair; the second call is a no-op) — rx untouched
+        before = c.checksum(rx, cap)
+        for _ in range(2):
+            c.prepare(mpx.MODE_NONBLOCKING, 0, 0, 0, 600, cap)
+        assert c.checksum(rx, cap) == before
         for n in (0, 1, 4097, 65541, cap):
             want = c.checksum(tx, n)
             for iters in (1, 255, 256, 257, 600):
