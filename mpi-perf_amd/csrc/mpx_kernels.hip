@@ -136,11 +136,11 @@ __global__ __launch_bounds__(kBlock) void k_copy(const v4u* __restrict__ src, v4
 // below 1 MiB).
 constexpr int kCopyStepsBatch = 8;
 
-template <bool XCD>
-__global__ __launch_bounds__(kBlock) void k_copy_steps(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n16,
-                                                      unsigned tail, int iters, u64* bar, int drain) {
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    const size_t first = (size_t)blockIdx.x * kBlock + threadIdx.x;
+template <int T, bool XCD>
+__global__ __launch_bounds__(T) void k_copy_steps(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n16,
+                                                 unsigned tail, int iters, u64* bar, int drain) {
+    const size_t stride = (size_t)gridDim.x * T;
+    const size_t first = (size_t)blockIdx.x * T + threadIdx.x;
     const u64 g = gridDim.x;
     // XCD = true: two-level arrival.  Workgroups are dispatched round-robin
     // over the 8 XCDs, so workgroup b counts in on its XCD's counter
@@ -928,26 +928,38 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
     // Defaults from the A/Bs: at most 64 workgroups and one hot counter
     // (fewer arrivals beat more lanes: 1 MiB 2.08 us vs 2.40 with 256,
     // profiles/r02_copy_steps_variants.jsonl); no store drain before arrival
-    // (the barrier orders issue, not acknowledgement: -0.05..0.1 us per step);
-    // the grid sized for `upl` 16-B units per lane per step, all of a lane's
-    // loads in flight at once: 1 up to 128 KiB, 4 at 256-512 KiB, 8 above (profiles/r02_copy_steps_upl.jsonl: 512 KiB 2.14 ->
-    // 1.82 us, 1 MiB 2.20 -> 2.02 against one unit per lane; below 256 KiB
-    // the two bench sweeps disagreed by more than the A/B's difference).
-    // MPX_COPY_STEPS="grid_cap:xcd:drain:upl" overrides (A/B knobs, read per call).
-    int cap = 64, xcd = 0, drain = 0;
-    int upl = n <= ((size_t)128 << 10) ? 1 : n <= ((size_t)512 << 10) ? 4 : 8;
-    if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d:%d", &cap, &xcd, &drain, &upl);
-    if (cap < 1 || cap > kCopyStepsMaxGrid) cap = kCopyStepsMaxGrid;
+    // (the barrier orders issue, not acknowledgement: -0.05..0.1 us per step).
+    // Workgroups of 1024 lanes, one unit per lane: 16 KiB per workgroup per
+    // step, so up to 16 KiB a copy is ONE workgroup and its steps need no
+    // grid barrier (__syncthreads ends a step), and up to 1 MiB at most 64
+    // workgroups arrive at the barrier.  Against the 256-lane grid sized for
+    // 1-8 units per lane: 8 KiB 0.96 -> 0.62 us per copy, 16 KiB 0.99 ->
+    // 0.70, 32-64 KiB 1.29-1.34 -> 1.12-1.15, 256-512 KiB 1.71-1.86 ->
+    // 1.48-1.67, 128 KiB and 1 MiB unchanged; one wide workgroup with more
+    // units per lane loses from 32 KiB (one CU's bandwidth)
+    // (profiles/r02_copy_steps_wgsize.jsonl).
+    // MPX_COPY_STEPS="grid_cap:xcd:drain:upl:threads" overrides (A/B knobs,
+    // read per call; threads = lanes per workgroup, 256 / 512 / 1024).
+    int cap = 64, xcd = 0, drain = 0, threads = 1024, upl = 1;
+    if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d:%d:%d", &cap, &xcd, &drain, &upl, &threads);
+    if (threads != 512 && threads != 1024) threads = kBlock;
+    // the grid barrier needs every workgroup resident: at most the waves of
+    // kCopyStepsMaxGrid 256-lane workgroups (4 per CU), whatever the width
+    const int max_grid = kCopyStepsMaxGrid * kBlock / threads;
+    if (cap < 1 || cap > max_grid) cap = max_grid;
     if (upl < 1) upl = 1;
     const size_t n16 = n / 16;
-    size_t grid = (n16 + (size_t)kBlock * upl - 1) / ((size_t)kBlock * upl);
+    size_t grid = (n16 + (size_t)threads * upl - 1) / ((size_t)threads * upl);
     if (grid > (size_t)cap) grid = (size_t)cap;
     if (grid < 1) grid = 1;
     if (grid_out) *grid_out = (int)grid;
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
-    hipLaunchKernelGGL(xcd ? k_copy_steps<true> : k_copy_steps<false>, dim3((unsigned)grid), dim3(kBlock), 0, s,
-                       reinterpret_cast<const v4u*>(src), reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters,
-                       bar, drain);
+    void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*, int) =
+        threads == 1024 ? (xcd ? k_copy_steps<1024, true> : k_copy_steps<1024, false>)
+        : threads == 512 ? (xcd ? k_copy_steps<512, true> : k_copy_steps<512, false>)
+                         : (xcd ? k_copy_steps<kBlock, true> : k_copy_steps<kBlock, false>);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3((unsigned)threads), 0, s, reinterpret_cast<const v4u*>(src),
+                       reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters, bar, drain);
     return hipGetLastError();
 }
 

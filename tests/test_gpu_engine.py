@@ -43,22 +43,26 @@ def test_fill_and_checksum_match_oracle(ctx, n, pattern):
 
 
 @pytest.mark.parametrize("iters", [1, 2, 7])
-@pytest.mark.parametrize("n", [1, 4096 + 5, (128 << 10) + 1, (512 << 10) + 7, (1 << 20), (1 << 20) + 3, (2 << 20) + 16,
-                               (8 << 20) + 1])
+@pytest.mark.parametrize("n", [1, 4096 + 5, 16 << 10, (16 << 10) + 1, (128 << 10) + 1, (512 << 10) + 7, (1 << 20),
+                               (1 << 20) + 3, (2 << 20) + 16, (8 << 20) + 1])
 def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
     """k_copy_steps (all copies in one launch, grid barrier between steps),
     forced at every size (MPX_COPY_STEPS_MAX): the grid classes of its
-    defaults (one workgroup; <= 64 workgroups with 1, 4 or 8 units per lane
-    and per-lane load batches) on both sides of each class boundary and of
-    the 1 MiB default threshold, plus the A/B knob combinations (grid cap,
-    per-XCD counters, drain, units per lane) at 1 MiB + 3: output against the
-    oracle's pattern, nothing written past the end."""
+    defaults (1024-lane workgroups, one unit per lane: one workgroup up to
+    16 KiB, <= 64 workgroups up to 1 MiB, then several units per lane in load
+    batches) on both sides of each class boundary and of the 1 MiB default
+    threshold, plus the A/B knob combinations (grid cap — clamped to what
+    stays resident —, per-XCD counters, drain, units per lane, 256 / 512 /
+    1024 lanes) at 1 MiB + 3: output against the oracle's pattern, nothing
+    written past the end."""
     monkeypatch.setenv("MPX_COPY_STEPS_MAX", str(16 << 20))
     key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
     try:
         ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
-        variants = [None] + (["64:0:1:1", "256:1:1:8", "1024:1:0:2", "1:0:0:1", "64:0:0:8", "16:0:0:3"]
+        variants = [None] + (["64:0:1:1:256", "256:1:1:8:256", "1024:1:0:2:256", "1:0:0:1:256", "64:0:0:8:256",
+                              "16:0:0:3:256", "64:0:0:1:512", "1:0:0:8:1024", "2:1:1:3:1024", "1024:0:0:1:1024",
+                              "9:1:0:1:1024"]
                              if n == (1 << 20) + 3 else [])
         for v in variants:
             if v:
