@@ -147,9 +147,13 @@ hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int*
 // must be 0 at launch
 constexpr int kCopyStepsMaxGrid = 1024;   // 4 workgroups per CU: always co-resident
 // copies up to 1 MiB run as k_copy_steps: faster than a launch per copy
-// there (1 MiB 2.0-2.7 vs 3.0-3.2 us); from 2 MiB a launch per copy is as fast
-// or faster (2 MiB 2.52 vs 2.78-3.01 us, 16 MiB 4.22 vs 5.15-5.95;
-// profiles/r02_copy_steps_upl.jsonl, r02_copy_steps_mid.jsonl)
+// there (1 MiB 1.94-2.0 vs 2.4-2.7 us).  At 2 MiB one launch is faster in a
+// fresh process (2.32-2.38 vs 2.42-2.94 us with 64 workgroups on one barrier
+// counter, on three boxes) but bistable: after bench.py's headline and sweep
+// it read 3.4-3.9 us on two boxes where a launch per copy read 2.6-3.0
+// (profiles/r02_copy_steps_wgsize_mid.jsonl, r02_copy_sweep_state.jsonl), so
+// the switch stays at 1 MiB; above it a launch per copy is as fast or faster
+// (16 MiB 4.22 vs 5.15-5.95; r02_copy_steps_upl.jsonl, r02_copy_steps_mid.jsonl)
 constexpr size_t kCopyStepsDefaultMax = (size_t)1 << 20;
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
                              int* grid_out);

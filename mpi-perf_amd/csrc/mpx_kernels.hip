@@ -937,10 +937,21 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
     // 0.70, 32-64 KiB 1.29-1.34 -> 1.12-1.15, 256-512 KiB 1.71-1.86 ->
     // 1.48-1.67, 128 KiB and 1 MiB unchanged; one wide workgroup with more
     // units per lane loses from 32 KiB (one CU's bandwidth)
-    // (profiles/r02_copy_steps_wgsize.jsonl).
+    // (profiles/r02_copy_steps_wgsize.jsonl).  Above 1 MiB (only when
+    // MPX_COPY_STEPS_MAX raises the switch) the 64 workgroups are 256 lanes
+    // with 8 units per lane, all loads of a step in flight at once: 2 MiB
+    // 2.35 us against 2.56-3.07 with 1024 lanes x 2
+    // (r02_copy_steps_wgsize_mid.jsonl, r02_copy_sweep_state.jsonl).
+    // Default-policy loads instead of nontemporal ones change nothing here,
+    // fresh or after 1 GiB copies evicted src (r02_copy_steps_ldpolicy.jsonl,
+    // measured with a knob since removed).
     // MPX_COPY_STEPS="grid_cap:xcd:drain:upl:threads" overrides (A/B knobs,
     // read per call; threads = lanes per workgroup, 256 / 512 / 1024).
     int cap = 64, xcd = 0, drain = 0, threads = 1024, upl = 1;
+    if (n > ((size_t)1 << 20)) {
+        threads = kBlock;
+        upl = 8;
+    }
     if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d:%d:%d", &cap, &xcd, &drain, &upl, &threads);
     if (threads != 512 && threads != 1024) threads = kBlock;
     // the grid barrier needs every workgroup resident: at most the waves of

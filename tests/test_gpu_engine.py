@@ -16,7 +16,7 @@ from pairs import Pairs
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [0, 1, 7, 8, 15, 16, 17, 255, 4095, 4096, 65537, (1 << 20) + 3, (64 << 20) + 13]
+SIZES = [0, 1, 7, 8, 15, 16, 17, 255, 4095, 4096, 65537, (1 << 20) + 3, (2 << 20) + 5, (64 << 20) + 13]
 GOLDEN = {c["name"]: c for c in O.golden()["cases"]}
 
 
@@ -49,12 +49,12 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
     """k_copy_steps (all copies in one launch, grid barrier between steps),
     forced at every size (MPX_COPY_STEPS_MAX): the grid classes of its
     defaults (1024-lane workgroups, one unit per lane: one workgroup up to
-    16 KiB, <= 64 workgroups up to 1 MiB, then several units per lane in load
-    batches) on both sides of each class boundary and of the 1 MiB default
-    threshold, plus the A/B knob combinations (grid cap — clamped to what
-    stays resident —, per-XCD counters, drain, units per lane, 256 / 512 /
-    1024 lanes) at 1 MiB + 3: output against the oracle's pattern, nothing
-    written past the end."""
+    16 KiB, <= 64 workgroups up to 1 MiB; 64 256-lane workgroups with 8
+    units per lane above, in load batches) on both sides of each class
+    boundary and of the 1 MiB default threshold, plus the A/B knob
+    combinations (grid cap — clamped to what stays resident —, per-XCD
+    counters, drain, units per lane, 256 / 512 / 1024 lanes) at 1 MiB + 3:
+    output against the oracle's pattern, nothing written past the end."""
     monkeypatch.setenv("MPX_COPY_STEPS_MAX", str(16 << 20))
     key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)

@@ -1,7 +1,20 @@
-"""k_copy_steps load policy at config 2's small sizes: nontemporal loads
-(default) against default-policy loads that can stay in the XCD's L2 across
-the copies of one call (MPX_COPY_STEPS 5th field), with the default grid
-rule.  One process, interleaved, best of 5 calls of 10 copies, two passes."""
+"""k_copy_steps load policy: nontemporal loads against default-policy loads
+(MPX_COPY_STEPS 6th field: the knob and its kernel variant were removed after
+this A/B found no difference), each with the default grid rule for the size,
+in two cache states:
+
+  fresh  — right after the buffers were filled (src resident in L2 / MALL);
+  after  — after a run of 1 GiB copies (bench.py's state when its sweep
+           starts: the headline's streaming copies have evicted src).
+
+The question: whether nontemporal loads, if they did not allocate on a miss,
+would make every repeated copy of an evicted small src pay HBM latency.  They
+do not: both policies read the same in both states.
+One process, interleaved, best of 5 calls of 10 copies, output checked.
+JSON lines.
+
+    python tools/copy_steps_ldpolicy.py > gpurun_out/copy_steps_ldpolicy.jsonl
+"""
 import json
 import os
 import sys
@@ -10,26 +23,34 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 import mpx  # noqa: E402
 
-
-def rule(n):   # launch_copy_steps' defaults
-    return 1 if n <= (128 << 10) else 4 if n <= (512 << 10) else 8
+G = 1 << 30
 
 
-top = 1 << 20
+def spec(n: int, ldnt: int) -> str:
+    return f"64:0:0:1:1024:{ldnt}" if n <= (1 << 20) else f"64:0:0:8:256:{ldnt}"
+
+
+SIZES = [4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 3 << 19, 2 << 20]
 with mpx.Context(1) as c:
-    a, b = c.alloc(0, top), c.alloc(0, top)
-    c.fill(a, top, mpx.FILL_SPLITMIX, 5)
-    for n in [1 << k for k in (0, 4, 8, 12, 13, 14, 16, 17, 18, 19, 20)]:
-        best = {}
-        for _ in range(2):
-            for ld in (1, 0):
-                os.environ["MPX_COPY_STEPS"] = f"64:0:0:{rule(n)}:{ld}"
-                c.copy(0, b, a, n, 2)
-                for _ in range(5):
-                    t = c.copy(0, b, a, n, 10)
-                    per = t.device_s / 10
-                    if ld not in best or per < best[ld]:
-                        best[ld] = per
-            assert c.checksum(b, n) == c.checksum(a, n), n
-        print(json.dumps(dict(bytes=n, nt_loads_us=round(best[1] * 1e6, 3), plain_loads_us=round(best[0] * 1e6, 3))),
-              flush=True)
+    src, dst = c.alloc(0, G), c.alloc(0, G)
+    c.fill(src, G, mpx.FILL_SPLITMIX, 5)
+    os.environ["MPX_COPY_STEPS_MAX"] = str(2 << 20)
+    for state in ("fresh", "after"):
+        if state == "after":
+            c.copy(0, dst, src, G, 30)
+        for n in SIZES:
+            best = {}
+            for _ in range(2):
+                for ldnt in (1, 0):
+                    if state == "after":
+                        c.copy(0, dst, src, G, 3)    # evict again before each variant
+                    os.environ["MPX_COPY_STEPS"] = spec(n, ldnt)
+                    c.copy(0, dst, src, n, 2)
+                    for _ in range(5):
+                        per = c.copy(0, dst, src, n, 10).device_s / 10
+                        if ldnt not in best or per < best[ldnt]:
+                            best[ldnt] = per
+            assert c.checksum(dst, n) == c.checksum(src, n), n
+            for ldnt, per in best.items():
+                print(json.dumps(dict(state=state, bytes=n, loads="nontemporal" if ldnt else "default",
+                                      us_per_copy=round(per * 1e6, 3))), flush=True)

@@ -7,6 +7,7 @@ passes, output checked.  JSON lines.
 
     python tools/copy_steps_wgsize.py > gpurun_out/copy_steps_wgsize.jsonl
     python tools/copy_steps_wgsize.py confirm    # the chosen default vs the old rule, 3 passes
+    python tools/copy_steps_wgsize.py mid        # 1-4 MiB: one launch (widths) vs a launch per copy
 
 "old" is the earlier default: 256-lane workgroups, grid <= 64, sized for 1
 unit per lane up to 128 KiB, 4 at 256-512 KiB and 8 above.
@@ -19,19 +20,30 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 import mpx  # noqa: E402
 
-CONFIRM = len(sys.argv) > 1 and sys.argv[1] == "confirm"
-VARIANTS = ["default", "old", "64:0:0:2:1024", "64:0:0:1:512"] if CONFIRM else ["default", "1:0:0:8:256", "1:0:0:8:512", "1:0:0:8:1024", "1:0:0:16:1024", "1:0:0:32:1024",
-            "16:0:0:8:1024", "64:0:0:1:1024", "64:0:0:4:1024", "64:0:0:8:512"]
-top = 2 << 20
+MODE = sys.argv[1] if len(sys.argv) > 1 else ""
+CONFIRM = MODE == "confirm"
+MID = MODE == "mid"
+VARIANTS = (["default", "old", "64:0:0:2:1024", "64:0:0:1:512"] if CONFIRM else
+            ["launch", "default", "64:0:0:8:256", "64:0:0:4:512", "64:0:0:2:1024"] if MID else
+            ["default", "1:0:0:8:256", "1:0:0:8:512", "1:0:0:8:1024", "1:0:0:16:1024", "1:0:0:32:1024",
+             "16:0:0:8:1024", "64:0:0:1:1024", "64:0:0:4:1024", "64:0:0:8:512"])
+top = (4 << 20) if MID else (2 << 20)
 with mpx.Context(1) as c:
-    a, b = c.alloc(0, top), c.alloc(0, top)
-    c.fill(a, top, mpx.FILL_SPLITMIX, 5)
+    # AB_ALLOC=bytes: allocate larger buffers (bench.py copies the first B
+    # bytes of 1 GiB ones) while copying the same sizes
+    alloc = max(top, int(os.environ.get("AB_ALLOC", "0")))
+    a, b = c.alloc(0, alloc), c.alloc(0, alloc)
+    c.fill(a, alloc, mpx.FILL_SPLITMIX, 5)
     os.environ["MPX_COPY_STEPS_MAX"] = str(top)
-    for n in ([1, 64, 1024] if CONFIRM else []) + [1 << k for k in range(12, 22)] + [(64 << 10) + 13]:
+    sizes = ([1, 64, 1024] if CONFIRM else []) + [1 << k for k in range(12, 22)] + [(64 << 10) + 13]
+    if MID:
+        sizes = [32 << 10, 1 << 20, 3 << 19, 2 << 20, 3 << 20, 4 << 20]
+    for n in sizes:
         best = {}
-        for _ in range(3 if CONFIRM else 2):
+        for _ in range(3 if CONFIRM or MID else 2):
             for v in VARIANTS:
                 os.environ.pop("MPX_COPY_STEPS", None)
+                os.environ["MPX_COPY_STEPS_MAX"] = "0" if v == "launch" else str(top)
                 if v == "old":
                     upl = 1 if n <= (128 << 10) else 4 if n <= (512 << 10) else 8
                     os.environ["MPX_COPY_STEPS"] = f"64:0:0:{upl}:256"
