@@ -138,19 +138,25 @@ constexpr int kCopyStepsBatch = 8;
 
 template <int T, bool XCD>
 __global__ __launch_bounds__(T) void k_copy_steps(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n16,
-                                                 unsigned tail, int iters, u64* bar, int drain) {
-    const size_t stride = (size_t)gridDim.x * T;
-    const size_t first = (size_t)blockIdx.x * T + threadIdx.x;
-    const u64 g = gridDim.x;
+                                                 unsigned tail, int iters, u64* bar, int drain, int one_xcd) {
+    // one_xcd (A/B): the grid is 8x the working workgroups and only those
+    // dispatched to XCD 0 (blockIdx % 8 == 0, round-robin dispatch) work, so
+    // every barrier arrival comes from one XCD; the rest exit at once
+    if (one_xcd && (blockIdx.x & 7)) return;
+    const unsigned wg = one_xcd ? blockIdx.x >> 3 : blockIdx.x;
+    const u64 g = one_xcd ? gridDim.x >> 3 : gridDim.x;
+    const size_t stride = (size_t)g * T;
+    const size_t first = (size_t)wg * T + threadIdx.x;
     // XCD = true: two-level arrival.  Workgroups are dispatched round-robin
     // over the 8 XCDs, so workgroup b counts in on its XCD's counter
     // bar[16 * (1 + b % 8)] (8 counters, 128 B apart, in parallel instead of
     // one hot word); the last arriver of each XCD then counts that XCD in on
     // bar[0].
-    const int x = (int)(blockIdx.x & 7);
+    const int x = (int)(wg & 7);
     const u64 nx = (g - (u64)x + 7) / 8;            // workgroups on this XCD
     const u64 groups = g < 8 ? g : 8;
     const bool one_unit = n16 <= stride;   // at most one unit per lane: no batch
+    __shared__ int s_stop;
     for (int s = 0; s < iters; ++s) {
         if (one_unit) {
             if (first < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(src + first), dst + first);
@@ -163,7 +169,7 @@ __global__ __launch_bounds__(T) void k_copy_steps(const v4u* __restrict__ src, v
             for (int u = 0; u < kCopyStepsBatch; ++u)
                 if (base + u * stride < n16) __builtin_nontemporal_store(r[u], dst + base + u * stride);
         }
-        if (blockIdx.x == 0 && threadIdx.x < tail) {
+        if (wg == 0 && threadIdx.x < tail) {
             const unsigned char* s8 = reinterpret_cast<const unsigned char*>(src + n16);
             reinterpret_cast<unsigned char*>(dst + n16)[threadIdx.x] = s8[threadIdx.x];
         }
@@ -172,6 +178,7 @@ __global__ __launch_bounds__(T) void k_copy_steps(const v4u* __restrict__ src, v
         __syncthreads();
         if (g == 1) continue;                       // one workgroup: __syncthreads is the barrier
         if (threadIdx.x == 0) {
+            s_stop = 0;
             u64 want;
             if constexpr (XCD) {
                 const u64 old = __hip_atomic_fetch_add(bar + 16 * (1 + x), 1ull, __ATOMIC_RELAXED,
@@ -183,10 +190,22 @@ __global__ __launch_bounds__(T) void k_copy_steps(const v4u* __restrict__ src, v
                 __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 want = g * (u64)(s + 1);
             }
-            while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want)
+            // bounded: the grid is sized to be resident, but a workgroup that
+            // never arrives must not hold the GPU: after 1 s the workgroup
+            // stops and flags bar[1], which mpx_copy reports as a timeout
+            const u64 t0 = now_ticks();
+            u64 spins = 0;
+            while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                if ((++spins & 255) == 0 && now_ticks() - t0 > 100000000ull) {
+                    __hip_atomic_store(&bar[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_stop = 1;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
+            }
         }
         __syncthreads();
+        if (s_stop) return;
     }
 }
 
@@ -945,18 +964,32 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
     // Default-policy loads instead of nontemporal ones change nothing here,
     // fresh or after 1 GiB copies evicted src (r02_copy_steps_ldpolicy.jsonl,
     // measured with a knob since removed).
-    // MPX_COPY_STEPS="grid_cap:xcd:drain:upl:threads" overrides (A/B knobs,
-    // read per call; threads = lanes per workgroup, 256 / 512 / 1024).
-    int cap = 64, xcd = 0, drain = 0, threads = 1024, upl = 1;
-    if (n > ((size_t)1 << 20)) {
+    // MPX_COPY_STEPS="grid_cap:xcd:drain:upl:threads:one_xcd" overrides (A/B
+    // knobs, read per call; threads = lanes per workgroup, 256 / 512 / 1024).
+    // One XCD: from 32 KiB to 512 KiB every working workgroup sits on XCD 0
+    // (8x the grid, the others exit at once), so the barrier's arrivals stay
+    // within one XCD: 32-64 KiB 1.16-1.20 -> 1.02 us per copy (512 lanes),
+    // 128 KiB 1.42 -> 1.12, 256 KiB 1.49 -> 1.25, 512 KiB 1.66 -> 1.53
+    // (1024 lanes); at 1 MiB XCD 0's 32 CUs are too few (2.12 vs 1.98)
+    // (profiles/r02_copy_steps_onexcd.jsonl).
+    int cap = 64, xcd = 0, drain = 0, threads = 1024, upl = 1, one_xcd = 0;
+    if (n > ((size_t)16 << 10) && n <= ((size_t)512 << 10)) {
+        one_xcd = 1;
+        threads = n <= ((size_t)128 << 10) ? 512 : 1024;
+    } else if (n > ((size_t)1 << 20)) {
         threads = kBlock;
         upl = 8;
     }
-    if (const char* v = getenv("MPX_COPY_STEPS")) sscanf(v, "%d:%d:%d:%d:%d", &cap, &xcd, &drain, &upl, &threads);
+    if (const char* v = getenv("MPX_COPY_STEPS"))
+        sscanf(v, "%d:%d:%d:%d:%d:%d", &cap, &xcd, &drain, &upl, &threads, &one_xcd);
     if (threads != 512 && threads != 1024) threads = kBlock;
     // the grid barrier needs every workgroup resident: at most the waves of
     // kCopyStepsMaxGrid 256-lane workgroups (4 per CU), whatever the width
-    const int max_grid = kCopyStepsMaxGrid * kBlock / threads;
+    int max_grid = kCopyStepsMaxGrid * kBlock / threads;
+    if (one_xcd) {           // the working workgroups share XCD 0's 32 CUs
+        max_grid /= 8;
+        xcd = 0;
+    }
     if (cap < 1 || cap > max_grid) cap = max_grid;
     if (upl < 1) upl = 1;
     const size_t n16 = n / 16;
@@ -965,12 +998,13 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
     if (grid < 1) grid = 1;
     if (grid_out) *grid_out = (int)grid;
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
-    void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*, int) =
+    void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*, int, int) =
         threads == 1024 ? (xcd ? k_copy_steps<1024, true> : k_copy_steps<1024, false>)
         : threads == 512 ? (xcd ? k_copy_steps<512, true> : k_copy_steps<512, false>)
                          : (xcd ? k_copy_steps<kBlock, true> : k_copy_steps<kBlock, false>);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3((unsigned)threads), 0, s, reinterpret_cast<const v4u*>(src),
-                       reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters, bar, drain);
+    hipLaunchKernelGGL(k, dim3((unsigned)(one_xcd ? grid * 8 : grid)), dim3((unsigned)threads), 0, s,
+                       reinterpret_cast<const v4u*>(src), reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters,
+                       bar, drain, one_xcd);
     return hipGetLastError();
 }
 

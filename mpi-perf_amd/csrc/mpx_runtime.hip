@@ -1212,6 +1212,12 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     HIPCK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    if (steps) {   // k_copy_steps gave up on its grid barrier (bar[1], see the kernel)
+        u64 stop = 0;
+        HIPCK(hipMemcpyAsync(&stop, bar + 1, sizeof stop, hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+        if (stop) return fail(MPX_ERR_TIMEOUT, "copy of %zu B: a workgroup never reached the step barrier", n);
+    }
     t->device_s = ms * 1e-3;
     t->bytes = (uint64_t)n * (uint64_t)iters;
     t->launches = !n ? 0 : steps ? 1 : iters;

@@ -53,7 +53,8 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
     units per lane above, in load batches) on both sides of each class
     boundary and of the 1 MiB default threshold, plus the A/B knob
     combinations (grid cap — clamped to what stays resident —, per-XCD
-    counters, drain, units per lane, 256 / 512 / 1024 lanes) at 1 MiB + 3:
+    counters, drain, units per lane, 256 / 512 / 1024 lanes, every working
+    workgroup on one XCD) at 1 MiB + 3:
     output against the oracle's pattern, nothing written past the end."""
     monkeypatch.setenv("MPX_COPY_STEPS_MAX", str(16 << 20))
     key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
@@ -62,7 +63,7 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
         ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
         variants = [None] + (["64:0:1:1:256", "256:1:1:8:256", "1024:1:0:2:256", "1:0:0:1:256", "64:0:0:8:256",
                               "16:0:0:3:256", "64:0:0:1:512", "1:0:0:8:1024", "2:1:1:3:1024", "1024:0:0:1:1024",
-                              "9:1:0:1:1024"]
+                              "9:1:0:1:1024", "32:0:0:1:1024:1", "64:1:1:2:512:1"]
                              if n == (1 << 20) + 3 else [])
         for v in variants:
             if v:

@@ -8,6 +8,7 @@ passes, output checked.  JSON lines.
     python tools/copy_steps_wgsize.py > gpurun_out/copy_steps_wgsize.jsonl
     python tools/copy_steps_wgsize.py confirm    # the chosen default vs the old rule, 3 passes
     python tools/copy_steps_wgsize.py mid        # 1-4 MiB: one launch (widths) vs a launch per copy
+    python tools/copy_steps_wgsize.py onexcd     # every working workgroup on XCD 0 (6th field)
 
 "old" is the earlier default: 256-lane workgroups, grid <= 64, sized for 1
 unit per lane up to 128 KiB, 4 at 256-512 KiB and 8 above.
@@ -23,7 +24,9 @@ import mpx  # noqa: E402
 MODE = sys.argv[1] if len(sys.argv) > 1 else ""
 CONFIRM = MODE == "confirm"
 MID = MODE == "mid"
-VARIANTS = (["default", "old", "64:0:0:2:1024", "64:0:0:1:512"] if CONFIRM else
+ONEXCD = MODE == "onexcd"
+VARIANTS = (["default", "prev", "64:0:0:1:1024:1", "64:0:0:1:512:1"] if ONEXCD else
+            ["default", "old", "64:0:0:2:1024", "64:0:0:1:512"] if CONFIRM else
             ["launch", "default", "64:0:0:8:256", "64:0:0:4:512", "64:0:0:2:1024"] if MID else
             ["default", "1:0:0:8:256", "1:0:0:8:512", "1:0:0:8:1024", "1:0:0:16:1024", "1:0:0:32:1024",
              "16:0:0:8:1024", "64:0:0:1:1024", "64:0:0:4:1024", "64:0:0:8:512"])
@@ -40,11 +43,13 @@ with mpx.Context(1) as c:
         sizes = [32 << 10, 1 << 20, 3 << 19, 2 << 20, 3 << 20, 4 << 20]
     for n in sizes:
         best = {}
-        for _ in range(3 if CONFIRM or MID else 2):
+        for _ in range(3 if CONFIRM or MID or ONEXCD else 2):
             for v in VARIANTS:
                 os.environ.pop("MPX_COPY_STEPS", None)
                 os.environ["MPX_COPY_STEPS_MAX"] = "0" if v == "launch" else str(top)
-                if v == "old":
+                if v == "prev":      # the default before the one-XCD rule: 1024 lanes, 1 unit, all XCDs
+                    os.environ["MPX_COPY_STEPS"] = "64:0:0:1:1024:0" if n <= (1 << 20) else "64:0:0:8:256:0"
+                elif v == "old":
                     upl = 1 if n <= (128 << 10) else 4 if n <= (512 << 10) else 8
                     os.environ["MPX_COPY_STEPS"] = f"64:0:0:{upl}:256"
                 elif v != "default":
