@@ -9,6 +9,7 @@ passes, output checked.  JSON lines.
     python tools/copy_steps_wgsize.py confirm    # the chosen default vs the old rule, 3 passes
     python tools/copy_steps_wgsize.py mid        # 1-4 MiB: one launch (widths) vs a launch per copy
     python tools/copy_steps_wgsize.py onexcd     # every working workgroup on XCD 0 (6th field)
+    python tools/copy_steps_wgsize.py hier       # 256 KiB - 1 MiB: per-XCD arrival counters (2nd field)
 
 "old" is the earlier default: 256-lane workgroups, grid <= 64, sized for 1
 unit per lane up to 128 KiB, 4 at 256-512 KiB and 8 above.
@@ -25,7 +26,9 @@ MODE = sys.argv[1] if len(sys.argv) > 1 else ""
 CONFIRM = MODE == "confirm"
 MID = MODE == "mid"
 ONEXCD = MODE == "onexcd"
-VARIANTS = (["default", "prev", "64:0:0:1:1024:1", "64:0:0:1:512:1"] if ONEXCD else
+HIER = MODE == "hier"
+VARIANTS = (["default", "64:1:0:1:1024:0", "64:1:0:2:1024:0", "64:1:0:4:256:0", "64:1:0:1:512:0"] if HIER else
+            ["default", "prev", "64:0:0:1:1024:1", "64:0:0:1:512:1"] if ONEXCD else
             ["default", "old", "64:0:0:2:1024", "64:0:0:1:512"] if CONFIRM else
             ["launch", "default", "64:0:0:8:256", "64:0:0:4:512", "64:0:0:2:1024"] if MID else
             ["default", "1:0:0:8:256", "1:0:0:8:512", "1:0:0:8:1024", "1:0:0:16:1024", "1:0:0:32:1024",
@@ -41,9 +44,11 @@ with mpx.Context(1) as c:
     sizes = ([1, 64, 1024] if CONFIRM else []) + [1 << k for k in range(12, 22)] + [(64 << 10) + 13]
     if MID:
         sizes = [32 << 10, 1 << 20, 3 << 19, 2 << 20, 3 << 20, 4 << 20]
+    if HIER:
+        sizes = [256 << 10, 512 << 10, 768 << 10, 1 << 20]
     for n in sizes:
         best = {}
-        for _ in range(3 if CONFIRM or MID or ONEXCD else 2):
+        for _ in range(3 if CONFIRM or MID or ONEXCD or HIER else 2):
             for v in VARIANTS:
                 os.environ.pop("MPX_COPY_STEPS", None)
                 os.environ["MPX_COPY_STEPS_MAX"] = "0" if v == "launch" else str(top)
