@@ -288,6 +288,38 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs) -> dic
     return rates
 
 
+LL_AB_SIZES = (1024, 4096, 8192)
+LL_AB_ITERS = 2000
+
+
+def ll_vs_bulk(mpx, torch, dist, c, rounds, rank, tx, rx, errs) -> dict:
+    """Where the LL protocol (data-tagged 8-B granules, one hop) stops paying
+    against bulk (payload + drained flag, 2 B less per granule): round 0's
+    pairs ping-pong at 1, 4 and 8 KiB with every message LL (MPX_LL_MAX =
+    8 KiB, the cross-GPU default) and every message bulk (MPX_LL_MAX = 0),
+    half round trip, max over ranks.  libmpx reads MPX_LL_MAX per call and
+    every rank sets it alike before each loop, so both ends of a pair agree.
+    Kernel engine only; evidence for the cross-GPU `ll_max` choice."""
+    g, peer = round_role(rounds, 0, rank)
+    old = os.environ.get("MPX_LL_MAX")
+    out = {}
+    try:
+        for n in LL_AB_SIZES:
+            for proto, v in (("ll", "8192"), ("bulk", "0")):
+                os.environ["MPX_LL_MAX"] = v
+                dist.barrier()
+                w = torch.tensor([safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, LL_AB_ITERS, tx, rx, n)],
+                                 dtype=torch.float64)
+                dist.all_reduce(w, op=dist.ReduceOp.MAX)
+                out[f"{proto}_{n}"] = finite(float(w[0]) / (2 * LL_AB_ITERS) * 1e6, 3)
+    finally:
+        if old is None:
+            os.environ.pop("MPX_LL_MAX", None)
+        else:
+            os.environ["MPX_LL_MAX"] = old
+    return out
+
+
 # bulk push variants tuned on the node's own links: (workgroups per push,
 # streaming hint on the payload stores, mpx_xfer_opts.flags MPX_XFER_STREAM)
 PUSH_CANDIDATES = tuple((w, st) for w in (16, 32, 64, 128, 256) for st in (False, True))
@@ -598,6 +630,8 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         out["pingpong_8B_half_rtt_us"] = finite(float(lat[0]) / (2 * LATENCY_ITERS) * 1e6, 3)
         out["pair_pingpong_8B_half_rtt_us"] = pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs)
         out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs)
+        if engine == "kernel":
+            out["ll_vs_bulk_half_rtt_us"] = ll_vs_bulk(mpx, torch, dist, c, rounds, rank, tx, rx, errs)
         if nbytes >= HBV3_BYTES:
             out["hbv3_rounds"] = hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs)
         every = [None] * world
@@ -810,6 +844,8 @@ def main() -> None:
             extras["small_message_check"] = res["small_message_check"]
         if "hbv3_rounds" in res:
             extras["hbv3_rounds_unidir"] = res["hbv3_rounds"]
+        if "ll_vs_bulk_half_rtt_us" in res:
+            extras["ll_vs_bulk_half_rtt_us"] = res["ll_vs_bulk_half_rtt_us"]
         if "round0_sweep" in res:
             extras["round0_sweep"] = res["round0_sweep"]
             bidir = res["round0_sweep"].get(f"nonblocking_{nbytes}")

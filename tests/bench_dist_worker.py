@@ -97,7 +97,7 @@ class FakeMpx:
             if scenario == "latency_fails" and rank == 1 and mode == 0 and n == 8:
                 raise FakeError("device-side wait timed out (LL ping-pong)")
             FakeMpx.log.append(["xfer", self.engine, mode, group, me, peer, iters, n, bool(check_payload), expect,
-                                expect_ack, nwg, stream])
+                                expect_ack, nwg, stream, os.environ.get("MPX_LL_MAX")])
             time.sleep(0.002)
             if nwg and not check_payload and iters == 40:
                 # push tuning: rank 0 is fastest at 32, rank 1 slow at 32; the
@@ -128,6 +128,7 @@ if __name__ == "__main__":
     except SystemExit as e:
         out.update(exit=str(e))
     out["log"] = FakeMpx.log
+    out["ll_max_after"] = os.environ.get("MPX_LL_MAX")
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
     dist.barrier()

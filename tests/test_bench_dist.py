@@ -89,18 +89,25 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
     # then every round's pairs with 10^4, then the round-0 size sweep (config 3: unidir and full-duplex -x 1)
     for d in res:
         r = d["rank"]
-        pp = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0 and not x[8]]
+        pp_all = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0 and not x[8]]
+        pp, llab = pp_all[:world], pp_all[world:]
         assert len(pp) == world and pp[0][6] == 100_000 and pp[0][7] == 8
         # then 10^4 iterations of 8 B on every round: every pair's latency
         for rd, x in enumerate(pp[1:]):
             assert (x[3], x[5], x[6], x[7]) == (*round_role(rounds, rd, r), 10_000, 8)
         g, peer = round_role(rounds, 0, r)
-        sweep = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel" and not x[8]][warmup + steps + world:]
         sizes = [1, 8, 64, 512, 4096]                        # config 3's sizes <= B (B = 4096 here)
+        sweep = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel" and not x[8]][
+            warmup + steps + world:warmup + steps + world + 2 * len(sizes)]
         assert [x[7] for x in sweep] == [m for m in sizes for _ in (0, 1)]
         assert [x[2] for x in sweep] == [2, 1] * len(sizes)  # -u 1 then -x 1 at every size
         assert all((x[3], x[5]) == (g, peer) for x in sweep)
         assert set(d["res"]["round0_sweep"]) == {f"{m}_{k}" for k in sizes for m in ("unidir", "nonblocking")}
+        # then LL against bulk on round 0: ping-pong at 1/4/8 KiB, MPX_LL_MAX set alike on every rank per loop
+        assert [(x[7], x[13]) for x in llab] == [(m, v) for m in (1024, 4096, 8192) for v in ("8192", "0")]
+        assert all((x[3], x[5], x[6]) == (g, peer, 2000) for x in llab)
+        assert set(d["res"]["ll_vs_bulk_half_rtt_us"]) == {f"{p}_{m}" for m in (1024, 4096, 8192) for p in ("ll", "bulk")}
+        assert d["ll_max_after"] is None                     # the worker's environment is restored
 
 
 def test_ipc_failure_on_one_rank_falls_back_to_rccl_on_every_rank(tmp_path):
