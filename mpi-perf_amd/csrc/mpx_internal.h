@@ -114,7 +114,8 @@ struct XferArgs {
 
 // LL threshold of a link.  Within one GPU the bulk path's extra hop (payload
 // drain, then flag) is cheap and bulk wins above ~2 KiB (loopback sweep,
-// profiles/r01_loopback_sweep.jsonl); across xGMI that hop is a full link
+// profiles/r01_loopback_sweep.jsonl; on the final LL path ping-pong from
+// 3 KiB, r02_ll_threshold_ab.jsonl); across xGMI that hop is a full link
 // round trip, so LL is kept up to its 8 KiB landing zone.
 inline int ll_max_bytes(bool same_device) { return same_device ? 2048 : kLLMaxBytes; }
 
