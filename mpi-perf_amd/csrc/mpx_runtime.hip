@@ -315,7 +315,10 @@ bool plain_streams() {
 // context (the -m gpu suite: profiles/r02_stream_destroy_suite_hang.txt,
 // r02_stream_pool_ab.txt) unless the destroy waits ~50 ms after the drain —
 // the runtime still finishes a drained stream's last commands on its HSA
-// event thread (the exit stall below, same race).  So rank streams are
+// event thread (the exit stall below, same race).  A device-wide
+// hipDeviceSynchronize before each destroy, without the delay, does not
+// prevent it: the engine tests stalled after 161 passed, inside the next
+// context's first fill (profiles/r02_stream_destroy_devsync.txt).  So rank streams are
 // process-lifetime objects, like the runtime's own queues: mpx_finalize
 // drains them, frees every allocation of the context, and returns them to a
 // per-device pool that later contexts reuse; an exit handler destroys the
