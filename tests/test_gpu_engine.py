@@ -81,6 +81,25 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
         ctx.free(dst)
 
 
+@pytest.mark.parametrize("n,grid", [(1, 1), (4096, 1), (16 << 10, 1), ((16 << 10) + 1, 2), (32 << 10, 4),
+                                    (128 << 10, 16), ((128 << 10) + 16, 9), (512 << 10, 32), ((512 << 10) + 16, 33),
+                                    (1 << 20, 64)])
+def test_copy_steps_grid_rule(ctx, n, grid):
+    """The one-launch copy's default shape (mpx_kernels.hip launch_copy_steps):
+    one 1024-lane workgroup up to 16 KiB; 512-lane workgroups on one XCD to
+    128 KiB, 1024-lane ones on one XCD to 512 KiB; up to 64 1024-lane
+    workgroups over every XCD to 1 MiB.  timing.nwg = working workgroups."""
+    src, dst = ctx.alloc(0, n), ctx.alloc(0, n)
+    try:
+        ctx.fill(src, n, mpx.FILL_BYTE, 0x5C)
+        t = ctx.copy(0, dst, src, n, 3)
+        assert (mpx.PROTOCOLS[t.protocol], t.nwg) == ("copy_steps", grid)
+        assert ctx.checksum(dst, n) == ctx.checksum(src, n)
+    finally:
+        ctx.free(src)
+        ctx.free(dst)
+
+
 @pytest.mark.parametrize("n", SIZES)
 def test_copy_kernel_matches_oracle(ctx, n):
     key = mpx.pattern_key(mpx.PATTERN_SEED, 0, 0, n & 0xFFFF)
