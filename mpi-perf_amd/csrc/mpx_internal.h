@@ -127,6 +127,7 @@ __host__ __device__ inline unsigned ll_tag(u64 seq) {
 
 // Workgroups of a bulk push of `len` bytes.  Both sides of a link evaluate
 // this on the same inputs, so the receiver knows how many flags to expect.
+constexpr long long kMinPushChunk = 1024;   // bytes per pushing workgroup, at least (run_kernel)
 inline int bulk_nwg(long long len, bool same_device) {
     // ~32 KiB per workgroup across xGMI (enough 16-B stores in flight to
     // cover the link's bandwidth-delay product), 16 KiB within one GPU.

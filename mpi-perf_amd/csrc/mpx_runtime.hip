@@ -514,6 +514,11 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     }();
     a.nwg = (o && o->nwg > 0) ? o->nwg : env_nwg > 0 ? env_nwg : bulk_nwg(len, same_device(me, peer));
     if (a.nwg > kMaxPushWG) return fail(MPX_ERR_INVALID, "nwg %d > %d", a.nwg, kMaxPushWG);
+    // a width chosen for large pushes (the call's option, MPX_PUSH_WG) is not
+    // applied to small ones: at least kMinPushChunk bytes per workgroup (the
+    // size rule's chunks are 16-32 KiB, so it never narrows them).  Both
+    // sides compute it from the same width and length, so they agree.
+    a.nwg = (int)std::max<long long>(1, std::min<long long>(a.nwg, (len + kMinPushChunk - 1) / kMinPushChunk));
     a.check = (o && o->check) ? 1 : 0;
     static const bool env_stream = [] {
         const char* v = getenv("MPX_PUSH_STREAM");

@@ -154,9 +154,10 @@ def test_loopback_pair_every_payload(engine, mode):
 
 
 # (push workgroups, B): chunk = ceil(B / nwg) rounded up to 16 B; chunks of
-# <= 60 KiB are pushed from LDS (stage_tx), larger ones straight from HBM
+# <= 60 KiB are pushed from LDS (stage_tx), larger ones straight from HBM; a
+# width wider than B / 1 KiB is narrowed to that (run_kernel, kMinPushChunk)
 PUSH_CASES = [(1, 40000), (1, 70001), (7, 456131), (8, 456131), (33, (1 << 20) + 17), (128, (4 << 20) + 3),
-              (256, (20 << 20) + 5)]
+              (256, (20 << 20) + 5), (64, 20000), (256, 3000)]
 
 
 @pytest.mark.parametrize("stream", [False, True])
@@ -174,7 +175,7 @@ def test_push_widths_staged_and_unstaged(mode, stream):
             for r in (0, 1):
                 pushes = mode != mpx.MODE_UNIDIR or r == 0
                 if pushes:
-                    assert out[r].nwg == nwg and out[r].protocol == 1, (nwg, n, r)
+                    assert out[r].nwg == min(nwg, -(-n // 1024)) and out[r].protocol == 1, (nwg, n, r)
                 assert out[r].check_failures == 0 and out[r].check_iters == 5
                 m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else n
                 assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (nwg, n, r)
