@@ -11,7 +11,7 @@ A "step" is one run of the reference's loop (mpi_perf.c:474-569: barrier ->
   is `iters` launches of the HBM copy kernel moving B = 1 GiB tx -> rx (the
   loop's degenerate pair, both ends on one GPU).  value = B*iters*K / T.
   After the timed steps: config 2's sweep (1 B .. 1 GiB), the same copy held
-  for 6 s (sustained rate), loopback pair latency / rate, the runtime's copy.
+  for 10 s (sustained rate), loopback pair latency / rate, the runtime's copy.
 * N >= 2 — BASELINE config 4, all-pairs concurrent rounds (run-hbv3-style,
   unidirectional): step s runs round s mod (N-1) of the circle-method
   schedule; each of the N/2 pairs moves `iters` x 4 MiB G1 -> G0 over xGMI
@@ -152,7 +152,7 @@ def copy_sweep(mpx, c, src, dst, nbytes: int) -> dict:
     return out
 
 
-def sustained_copy(c, src, dst, nbytes: int, seconds: float = 6.0) -> dict:
+def sustained_copy(c, src, dst, nbytes: int, seconds: float = 10.0) -> dict:
     """The headline copy held for `seconds` of back-to-back launches (calls of
     300 copies, ~0.1 s each at 1 GiB): whether the rate of the short timed
     region holds once clocks and temperature settle.  HBM traffic (2B per
