@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 3
+#define MPX_ABI_VERSION 4
 #define MPX_MAX_RANKS 64          /* ranks one context can address           */
 #define MPX_RANK_DESC_BYTES 512   /* size of the opaque exported descriptor  */
 #define MPX_RCCL_ID_BYTES 128     /* size of an RCCL unique id               */

@@ -32,12 +32,22 @@ enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProt
 //                  {tag:32 | payload:32}, tag = ll_tag(seq), one 8-byte store
 //   credit[s][w] : non-blocking check mode only — sequence number of the last
 //                  of THIS rank's pushes whose chunk w rank s has checksummed
-//                  (and poisoned), i.e. the ring slot it used is free again;
-//                  rx_seq0 at the start of each of s's checked calls
+//                  (and poisoned), i.e. the ring slot it used is free again
+//   posted[s]    : "receives posted", written by rank s: the number of the
+//                  latest transfer call between s and this rank that s has
+//                  started.  It grows by one per call on both sides
+//                  (Rank.calls), so no call's value equals an earlier call's.
+//                  Rank s stores it as the first action of its call (its
+//                  stream has then finished all of its previous call's work);
+//                  this rank pushes no byte of call k into s's rx, ring or LL
+//                  zone before it reads posted[s] >= k.  That is MPI's
+//                  matched-receive order (mpi_perf.c:75,79,100,104,137,141):
+//                  a payload of call k lands only under a receive of call k.
 struct Mailbox {
     u64 flag[MPX_MAX_RANKS][kMaxPushWG];
     u64 ll[MPX_MAX_RANKS][kLLGranules];
     u64 credit[MPX_MAX_RANKS][kMaxPushWG];
+    u64 posted[MPX_MAX_RANKS];
 };
 
 // Per-rank host-mapped status words (written by the device, read by the host
@@ -110,6 +120,10 @@ struct XferArgs {
     int slots;                   // S: receive slots per link (ring_slots)
     int skip_push;               // test knob: 1 + iteration whose payload stores
                                  // are skipped (flag still published); 0 = off
+    u64 call;                    // number of this call on the link (Mailbox.posted)
+    int lag_wg;                  // test knob (MPX_TEST_LAG_WG): workgroup that stalls
+    u64 lag_ticks;               //   lag_ticks before checking the call's last
+                                 //   receive (non-blocking check mode); 0 = off
 };
 
 // LL threshold of a link.  Within one GPU the bulk path's extra hop (payload

@@ -523,6 +523,31 @@ struct Loop {
         return is_ll(n) ? wait_ll(n, seq, iter) : wait_bulk(seq, iter);
     }
 
+    // ---- matched-receive order (Mailbox.posted) -----------------------------
+    // This call's receives are posted: the peer may now push its call a.call
+    // into this rank's rx / ring / LL zone.  The kernel is the first command
+    // of the call on this rank's stream, so every workgroup of the previous
+    // call has finished (checks, poison stores and all) and the host has
+    // finished whatever it did with rx between the calls.
+    __device__ void post_receives() const {
+        if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(&a.peer_mb->posted[a.my_slot], a.call);
+    }
+    __device__ bool peer_posted() const { return ld_sys(&a.my_mb->posted[a.peer_slot]) >= a.call; }
+    // Before this side's first push of the call: wait for the peer's post.
+    // Once per call, not per iteration.
+    __device__ bool wait_posted() const {
+        if (threadIdx.x == 0) {
+            const u64 t0 = now_ticks();
+            u64 spins = 0;
+            while (!peer_posted()) {
+                if (should_stop(++spins, t0)) { give_up(0); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
+
     // ---- check mode: checksum the received payload, then poison it ----------
     // The poison guarantees the NEXT iteration's checksum only passes if the
     // next payload really overwrote every byte.
@@ -629,6 +654,15 @@ struct Loop {
     // the next payload.
     __device__ void check_nb(int j) const {
         const long long n = a.len;
+        if (a.lag_ticks && (int)blockIdx.x == a.lag_wg && j + 1 == a.iters) {
+            // test knob (MPX_TEST_LAG_WG): this workgroup is late to check the
+            // call's last receive, so the call ends well after the peer's
+            if (threadIdx.x == 0) {
+                const u64 t0 = now_ticks();
+                while (now_ticks() - t0 < a.lag_ticks) __builtin_amdgcn_s_sleep(127);
+            }
+            __syncthreads();
+        }
         const u64 poison = 0x5a5a5a5a5a5a5a5aull ^ (u64)j;
         const u64 acc = sum_chunk(slot_base(a.rx, a.ring, j), n, poison, j + 1 == a.iters);
         const u64 s = block_sum(acc, lds4);
@@ -731,7 +765,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     u64 txs = a.tx_seq0, rxs = a.rx_seq0;
     u64 done = 0;                                       // receives completed (Status.recv_done)
     int inflight = 0;
-    for (int i = 0; i < a.iters; ++i) {
+    L.post_receives();
+    // A side whose first action is a push waits for the peer's post.  Group 0
+    // of ping-pong / unidir pushes only after its first receive, which the
+    // peer sent after it saw this side's post, so its peer has started too.
+    constexpr bool push_first = MODE == MPX_MODE_NONBLOCKING || GROUP == 1;
+    const bool go = !push_first || a.iters == 0 || L.wait_posted();
+    for (int i = 0; go && i < a.iters; ++i) {
         const bool skip = a.skip_push == i + 1;        // test knob only
         if constexpr (MODE == MPX_MODE_PINGPONG) {    // mpi_perf.c:70-82
             if constexpr (GROUP == 1) {
@@ -816,19 +856,26 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     if (a.stage) L.stage_tx(n);
     __syncthreads();
     const int w = blockIdx.x;
-    // this call starts: every push of the peer before it has been consumed
-    if (threadIdx.x == 0) st_sys(&a.peer_mb->credit[a.my_slot][w], a.rx_seq0);
     const u64 fmix = mix64((u64)n);
     const u64* credit = &a.my_mb->credit[a.peer_slot][w];
     int next = 0, inflight = 0;
     u64 done = 0, dig = 0;
-    bool ok = true;
+    // The peer's receive slots are free for this call only once the peer's
+    // kernel of this call runs (Mailbox.posted): its previous kernel — every
+    // workgroup's checks and poison stores of the previous call, whatever
+    // that call's length, width and slot layout — has finished by then.
+    // Credits alone cannot say so: they are per workgroup, and the previous
+    // call's last credits already satisfy this call's first S pushes.
+    L.post_receives();
+    bool ok = a.iters == 0 || L.nb_wait([&] { return threadIdx.x != 0 || L.peer_posted(); }, &next, 0);
     for (int i = 0; i < a.iters && ok; ++i) {
-        // slot ring_slot(i) was last used by push i - S: wait for its credit
-        // (and, for the first S pushes, for the peer to have started)
-        const u64 want = a.tx_seq0 + (u64)(i >= a.slots ? i - a.slots + 1 : 0);
-        ok = L.nb_wait([&] { return threadIdx.x != 0 || ld_sys(credit) >= want; }, &next, i);
-        if (!ok) break;
+        // slot ring_slot(i) was last used by push i - S of this call: wait
+        // for its credit
+        if (i >= a.slots) {
+            const u64 want = a.tx_seq0 + (u64)(i - a.slots + 1);
+            ok = L.nb_wait([&] { return threadIdx.x != 0 || ld_sys(credit) >= want; }, &next, i);
+            if (!ok) break;
+        }
         L.push_bulk(n, a.tx_seq0 + (u64)i + 1, true, L.slot_base(a.peer_rx, a.peer_ring, i), a.skip_push == i + 1);
         if (inflight == kNbWindow - 1) {               // Waitall(255): iterations i-255 .. i-1
             ok = L.nb_wait([&] { return next >= i; }, &next, i);

@@ -115,6 +115,7 @@ struct Rank {
     std::vector<void*> retired;    // outgrown csum arrays (freed at finalize)
     u64 tx_seq[MPX_MAX_RANKS] = {};
     u64 rx_seq[MPX_MAX_RANKS] = {};
+    u64 calls[MPX_MAX_RANKS] = {};   // transfer calls on the link to that rank (Mailbox.posted)
     ncclComm_t comm = nullptr;
     int comm_rank = -1;
     bool rccl_linked[MPX_MAX_RANKS] = {};          // RCCL p2p channel to that rank set up (mpx_xfer_prepare)
@@ -288,6 +289,29 @@ u64 nb_waited(int iters) {
 int skip_push_knob() {
     const char* v = getenv("MPX_TEST_SKIP_PUSH");
     return v ? atoi(v) : 0;
+}
+
+// test knob (MPX_TEST_LAG_WG="rank:wg:us"): in non-blocking check mode,
+// workgroup wg of `rank` stalls `us` microseconds before it checks the call's
+// last receive, so that rank's call ends long after its peer's; read per call
+void lag_knob(int my_rank, int* wg, u64* ticks) {
+    *wg = 0;
+    *ticks = 0;
+    const char* v = getenv("MPX_TEST_LAG_WG");
+    int r = -1, w = 0;
+    long long us = 0;
+    if (v && sscanf(v, "%d:%d:%lld", &r, &w, &us) == 3 && r == my_rank && us > 0) {
+        *wg = w;
+        *ticks = (u64)us * 100ull;   // s_memrealtime: 100 MHz
+    }
+}
+
+// test knob (MPX_TEST_NO_POSTED=1): no receive-posted handshake (the sender
+// pushes call k+1 as soon as its own state allows, the round-2 behaviour);
+// the negative control of tests/test_gpu_ordering.py; read per call
+bool no_posted_knob() {
+    const char* v = getenv("MPX_TEST_NO_POSTED");
+    return v && atoi(v) != 0;
 }
 
 bool plain_streams() {
@@ -534,6 +558,7 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.cnt = me.cnt;
     a.slots = link_slots(me, peer, len);
     a.skip_push = skip_push_knob();
+    lag_knob(my_rank, &a.lag_wg, &a.lag_ticks);
     if (a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!me.ring || !peer.ring))
         return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
 
@@ -569,6 +594,10 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     me.status->recv_done = 0;
     me.status->recv_digest = 0;
 
+    // a call that moves nothing (iters = 0) posts nothing new: the count
+    // stays equal on both sides even if only one side makes such a call
+    a.call = iters > 0 ? ++me.calls[peer_rank] : me.calls[peer_rank];
+    if (no_posted_knob()) a.call = 0;   // every wait for posted >= 0 holds at once
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
     HIPCK(launch_xfer(a, grid, me.stream));
@@ -712,13 +741,14 @@ struct SdmaOps {
     // checksummed and poisoned right after this side's push i (so the two
     // streams never wait on each other in a cycle), and the device counts
     // the reference's Waitall receives (k_account at each flush).
+    // The call's receives were posted (Mailbox.posted) before it starts, so
+    // the first `slots` pushes need no credit.
     int nb_checked(int iters, long long len, u64 tx0, u64 rx0, int slots) {
         u64* credit_out = &peer.mb->credit[my_slot][0];
         const u64* credit_in = &me.mb->credit[peer_slot][0];
-        TRY(signal_abs(credit_out, rx0));            // this call starts
         int inflight = 0;
         for (int i = 0; i < iters; ++i) {
-            TRY(wait_abs(credit_in, tx0 + (u64)(i >= slots ? i - slots + 1 : 0)));
+            if (i >= slots) TRY(wait_abs(credit_in, tx0 + (u64)(i - slots + 1)));
             if (len > 0 && skip != i + 1) {
                 HIPCK(hipMemcpyAsync(slot_ptr(peer, i, iters, slots, len), me.tx, (size_t)len,
                                      sdma_kind(same_device(me, peer) && &me != &peer), me.stream));
@@ -827,6 +857,14 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     if (full || tail) HIPCK(launch_seqbase(me.scratch + kScrSeqBase, txs0, rxs0, 0, me.stream));
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
+    // matched-receive order (Mailbox.posted), stream-ordered: post this
+    // call's receives, and a side that pushes first waits for the peer's
+    // post before its first copy into the peer's rx
+    if (iters > 0 && !no_posted_knob()) {
+        const u64 call = ++me.calls[peer_rank];
+        TRY(op.signal_abs(&peer.mb->posted[my_rank], call));
+        if (mode == MPX_MODE_NONBLOCKING || group == 1) TRY(op.wait_abs(&me.mb->posted[peer_rank], call));
+    }
     if (check && mode == MPX_MODE_NONBLOCKING) {
         TRY(op.nb_checked(iters, len, txs0, rxs0, slots));
     } else {

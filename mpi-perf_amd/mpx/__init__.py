@@ -29,7 +29,7 @@ MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
 MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": MODE_UNIDIR}
 FILL_BYTE, FILL_SPLITMIX = 0, 1
 XFER_STREAM = 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 PATTERN_SEED = 0x6D70695F70657266
 MAX_RANKS = 64
 RANK_DESC_BYTES = 512

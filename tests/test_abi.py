@@ -28,7 +28,7 @@ def test_every_header_symbol_is_exported():
 
 def test_version_and_strerror():
     L = mpx.lib()
-    assert L.mpx_version() == 3   # 2: mpx_timing gained recv_done / recv_digest; 3: 64 ranks per context
+    assert L.mpx_version() == 4   # 2: recv_done / recv_digest; 3: 64 ranks per context; 4: receive-posted mailbox word
     texts = {L.mpx_strerror(i).decode() for i in range(9)}
     assert len(texts) == 9
     assert L.mpx_strerror(12345) == b"unknown mpx status"
