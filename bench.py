@@ -810,14 +810,13 @@ def main() -> None:
                     frac_of_bidirectional_link=round(achieved / XGMI_LINK_PEAK_BIDIR_GBPS, 4),
                     kernel="k_xfer (G1 side)" if engine_used == "kernel" else engine_used,
                     avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
-        prof = traffic_from_profile(workload)
-        if prof and prof.get("bytes") == nbytes and engine_used == "kernel":
-            # PMC bytes per push of the same kernel and B (loopback pair, one
-            # GPU), times the pushes of one launch: the sender's memory-side
-            # requests, wherever they land (local DRAM there, a peer's HBM
-            # over xGMI here)
-            roof["traffic"] = round(prof["hbm_bytes_per_push"] * iters)
-            roof["traffic_source"] = prof.get("source")
+        # Link bytes need PMC counters of THIS run's sender launches, which a
+        # process cannot collect on itself: tools/node_profile.sh starts every
+        # rank under its own rocprofv3 (sender TCC_EA0_WRREQ - WRREQ_DRAM, x 64 B
+        # per request) on a multi-GPU node.  A one-GPU loopback constant is no
+        # measurement of an xGMI link, so the line says "not measured".
+        roof["traffic_source"] = ("not measured at N>=2: per-rank link bytes come from tools/node_profile.sh "
+                                  "(rocprofv3 --pmc TCC_EA0_WRREQ/_DRAM per rank)")
         config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=engine_used,
                       rounds=world - 1, pairs_per_round=world // 2, parallelism=f"pairs{world // 2}",
                       validated_rounds=res["validated_rounds"], push=res.get("push", "default"))

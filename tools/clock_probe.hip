@@ -1,0 +1,46 @@
+// clock_probe.hip — diagnostic only (tools/copy_cliff.py): the shader clock
+// the GPU runs at right now, measured in a kernel as
+//   delta s_memtime (shader cycles) / delta s_memrealtime (100 MHz ticks)
+// over `ms` milliseconds of spinning (MI355X_MICROARCH.md "DVFS give-back",
+// item 6).  One workgroup per CU (`wgs` of them), every one stamping; the
+// host takes the median.  The stamps go to a buffer of their own.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <vector>
+
+typedef unsigned long long u64;
+
+__global__ void k_clock(u64* out, u64 ticks) {
+    if (threadIdx.x != 0) return;
+    const u64 r0 = __builtin_amdgcn_s_memrealtime();
+    const u64 c0 = __builtin_amdgcn_s_memtime();
+    u64 r1 = r0, c1 = c0;
+    while (r1 - r0 < ticks) {
+        __builtin_amdgcn_s_sleep(10);
+        r1 = __builtin_amdgcn_s_memrealtime();
+        c1 = __builtin_amdgcn_s_memtime();
+    }
+    out[2 * blockIdx.x] = c1 - c0;
+    out[2 * blockIdx.x + 1] = r1 - r0;
+}
+
+extern "C" int clock_probe(int dev, double ms, int wgs, double* ghz) {
+    if (hipSetDevice(dev) != hipSuccess || wgs < 1) return 1;
+    u64* d = nullptr;
+    if (hipMalloc(&d, 16 * (size_t)wgs) != hipSuccess) return 2;
+    static hipStream_t s = nullptr;   // one per process, never destroyed (diagnostic)
+    if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 3;
+    hipLaunchKernelGGL(k_clock, dim3(wgs), dim3(64), 0, s, d, (u64)(ms * 1e5));
+    std::vector<u64> h(2 * (size_t)wgs);
+    int rc = hipMemcpyAsync(h.data(), d, 16 * (size_t)wgs, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                     hipStreamSynchronize(s) == hipSuccess ? 0 : 4;
+    (void)hipFree(d);
+    if (rc) return rc;
+    std::vector<double> f;
+    for (int i = 0; i < wgs; ++i)
+        if (h[2 * i + 1]) f.push_back((double)h[2 * i] / (double)h[2 * i + 1] * 0.1);   // GHz
+    if (f.empty()) return 5;
+    std::nth_element(f.begin(), f.begin() + f.size() / 2, f.end());
+    *ghz = f[f.size() / 2];
+    return 0;
+}
