@@ -111,7 +111,7 @@ struct Rank {
     u64* cnt = nullptr;            //   then cnt: checked chunks per receive (csum + csum_cap)
     size_t csum_cap = 0;
     unsigned char* ring = nullptr; // non-blocking check mode's receive slots 1..S-1
-    uint64_t ring_bytes = 0;
+    uint64_t ring_bytes = 0;       //   (allocated on first use, or at export: ensure_ring)
     std::vector<void*> retired;    // outgrown csum arrays (freed at finalize)
     u64 tx_seq[MPX_MAX_RANKS] = {};
     u64 rx_seq[MPX_MAX_RANKS] = {};
@@ -256,6 +256,27 @@ uint64_t ring_bytes_for(size_t len) {
     const uint64_t want = (uint64_t)(kNbWindow - 1) * len;
     const uint64_t slots = (want < cap ? want : cap) / len;
     return slots * len;
+}
+
+// The check-mode receive ring of a local rank, allocated on its first use
+// (a non-blocking call in check mode, by either rank of the link) or when the
+// rank is exported: a peer process may push into it, and the descriptor
+// carries its IPC handle.  A job that never checks non-blocking payloads
+// never pays for it (up to 64 MiB per rank).  Caller holds ctx->mu.
+int ensure_ring(Rank& rk) {
+    if (!rk.local || rk.ring) return MPX_OK;
+    const uint64_t bytes = ring_bytes_for(rk.len);
+    if (!bytes) return MPX_OK;
+    DeviceGuard g(rk.dev);
+    HIPCK(g.err);
+    void* p = nullptr;
+    const hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipErrorOutOfMemory)
+        return fail(MPX_ERR_NOMEM, "check ring of %llu B on device %d", (unsigned long long)bytes, rk.dev);
+    HIPCK(e);
+    rk.ring = static_cast<unsigned char*>(p);
+    rk.ring_bytes = bytes;
+    return MPX_OK;
 }
 
 // receive slots of the link between two ranks: the same on both sides
@@ -434,7 +455,13 @@ int create_rank_stream(int dev, hipStream_t* s) {
 void destroy_stream_pool() {
     StreamPool& p = pool();
     std::lock_guard<std::mutex> lk(p.mu);
-    if (p.live_contexts != 0 || p.all.empty()) return;   // a context still owns memory they touched
+    // A context still alive at exit owns memory its streams' kernels touched:
+    // destroying the streams before that memory is freed is the order that
+    // hangs the runtime's exit teardown (above), and freeing it here could pull
+    // it from under another thread still inside a call.  So they are left to
+    // the runtime.  libmpx's own hosts never get here on a failure: MPX_CHECK
+    // flushes stdio and _exits (host/mpx_perf.c, integration/mpx_binding.c).
+    if (p.live_contexts != 0 || p.all.empty()) return;
     // The runtime finishes a drained stream's last commands on its HSA event
     // thread (completion callbacks) slightly after hipStreamSynchronize
     // returns.  Destroying the stream under a callback still in flight left
@@ -1242,28 +1269,36 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     int grid = 0;
     // copies of <= copy_steps_max() bytes run all iterations in one launch
     // (k_copy_steps: dispatch-bound sizes); larger ones one k_copy launch each
-    const bool steps = n && iters > 1 && n <= copy_steps_max();
+    bool steps = n && iters > 1 && n <= copy_steps_max();
     u64* bar = ctx->dev_tmp[dev] + 16;
-    if (steps) HIPCK(hipMemsetAsync(bar, 0, 9 * 16 * sizeof(u64), s));   // global + 8 per-XCD counters
-    const double t0 = now_s();
-    HIPCK(hipEventRecord(e0, s));
-    if (steps)
-        HIPCK(launch_copy_steps(dst, src, n, iters, bar, s, &grid));
-    else
-        for (int i = 0; i < iters && n; ++i) HIPCK(launch_copy(dst, src, n, s, &grid));
-    HIPCK(hipEventRecord(e1, s));
-    HIPCK(hipEventSynchronize(e1));
-    t->wall_s = now_s() - t0;
     float ms = 0;
-    HIPCK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (steps) {   // k_copy_steps gave up on its grid barrier (bar[1], see the kernel)
+    double t0 = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if (steps) HIPCK(hipMemsetAsync(bar, 0, 9 * 16 * sizeof(u64), s));   // global + 8 per-XCD counters
+        t0 = now_s();
+        HIPCK(hipEventRecord(e0, s));
+        if (steps)
+            HIPCK(launch_copy_steps(dst, src, n, iters, bar, s, &grid));
+        else
+            for (int i = 0; i < iters && n; ++i) HIPCK(launch_copy(dst, src, n, s, &grid));
+        HIPCK(hipEventRecord(e1, s));
+        HIPCK(hipEventSynchronize(e1));
+        HIPCK(hipEventElapsedTime(&ms, e0, e1));
+        if (!steps) break;
+        // k_copy_steps gave up on its grid barrier (bar[1], see the kernel):
+        // not every workgroup became resident — e.g. other ranks' persistent
+        // transfer kernels hold CUs of this GPU.  Copy again, a launch per copy
+        // (no residency needed); that is the call's result and its time.
         u64 stop = 0;
         HIPCK(hipMemcpyAsync(&stop, bar + 1, sizeof stop, hipMemcpyDeviceToHost, s));
         HIPCK(hipStreamSynchronize(s));
-        if (stop) return fail(MPX_ERR_TIMEOUT, "copy of %zu B: a workgroup never reached the step barrier", n);
+        if (!stop) break;
+        DBG("copy of %zu B: step barrier gave up, a launch per copy instead\n", n);
+        steps = false;
     }
+    t->wall_s = now_s() - t0;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     t->device_s = ms * 1e-3;
     t->bytes = (uint64_t)n * (uint64_t)iters;
     t->launches = !n ? 0 : steps ? 1 : iters;
@@ -1288,16 +1323,6 @@ int attach_resources(Rank& rk) {
     HIPCK(hipMalloc(&rk.scratch, kScratchWords * sizeof(u64)));
     HIPCK(hipMemsetAsync(rk.scratch, 0, kScratchWords * sizeof(u64), rk.stream));
     TRY(ensure_csum(rk, 1024));
-    // receive slots of non-blocking check mode (IPC-exportable like rx)
-    rk.ring_bytes = ring_bytes_for(rk.len);
-    if (rk.ring_bytes) {
-        void* p = nullptr;
-        const hipError_t e = hipMalloc(&p, rk.ring_bytes);
-        if (e == hipErrorOutOfMemory) return fail(MPX_ERR_NOMEM, "check ring of %llu B on device %d",
-                                                  (unsigned long long)rk.ring_bytes, rk.dev);
-        HIPCK(e);
-        rk.ring = static_cast<unsigned char*>(p);
-    }
     HIPCK(hipStreamSynchronize(rk.stream));
     return MPX_OK;
 }
@@ -1396,6 +1421,10 @@ int mpx_rank_export(mpx_ctx* ctx, int rank, void* desc) {
     DBG("export rank %d: rx %p mb %p (kind %d) dev %d\n", rank, (void*)rk.rx, (void*)rk.mb, rk.mb_kind, rk.dev);
     HIPCK(hipIpcGetMemHandle(&d.rx_handle, rk.rx));
     HIPCK(hipIpcGetMemHandle(&d.mb_handle, rk.mb));
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        TRY(ensure_ring(ctx->r[rank]));
+    }
     d.ring_bytes = rk.ring_bytes;
     if (rk.ring) HIPCK(hipIpcGetMemHandle(&d.ring_handle, rk.ring));
     memset(desc, 0, MPX_RANK_DESC_BYTES);
@@ -1468,6 +1497,13 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
         return fail(MPX_ERR_INVALID, "buff_len %d exceeds an attached length (%zu, %zu)", buff_len, me.len, peer.len);
     const int check = opts && opts->check;
     if (check) TRY(ensure_csum(me, iters));
+    if (check && mode == MPX_MODE_NONBLOCKING && ctx->engine != MPX_ENGINE_RCCL) {
+        // both ends of the link, under the lock: the other rank's thread may
+        // be here too, and both must see both rings before sizing the slots
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        TRY(ensure_ring(me));
+        TRY(ensure_ring(peer));
+    }
     DeviceGuard g(me.dev);
     HIPCK(g.err);
     int st;

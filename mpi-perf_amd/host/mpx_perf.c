@@ -60,13 +60,21 @@
 #include "mpx_host.h"
 
 /* MPI_CHECK analogue, mpi_perf.c:55-64: print and exit(EXIT_FAILURE) */
+/* A failed call ends the process at once, after flushing stdio (records and
+   messages written so far reach their files, as exit() would flush them):
+   _exit skips the atexit handlers and HIP's static destructors.  Other rank
+   threads may still be inside libmpx calls on the same context, so neither
+   finalizing the context here nor libmpx's exit handler can tear the rank
+   streams down safely; the kernel driver releases the GPU state of the
+   exiting process.  mpi_perf.c:55-64's MPI_CHECK exits EXIT_FAILURE too. */
 #define MPX_CHECK(stmt)                                                                                  \
     do {                                                                                                 \
         int mpx_errno = (stmt);                                                                          \
         if (MPX_OK != mpx_errno) {                                                                       \
             fprintf(stderr, "[%s:%d] mpx call failed with %d (%s: %s) \n", __FILE__, __LINE__, mpx_errno, \
                     mpx_strerror(mpx_errno), mpx_last_error());                                          \
-            exit(EXIT_FAILURE);                                                                          \
+            fflush(NULL);                                                                                \
+            _exit(EXIT_FAILURE);                                                                         \
         }                                                                                                \
     } while (0)
 

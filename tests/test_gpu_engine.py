@@ -516,35 +516,88 @@ def _self_rank(engine, cap):
     return c, tx, rx
 
 
+SELF_KEY = mpx.pattern_key(mpx.PATTERN_SEED, 0, 0, 7)   # _self_rank's tx pattern
+
+
 @pytest.mark.parametrize("engine", ["kernel", "sdma", "rccl"])
 def test_self_pair_nonblocking_every_payload(engine):
     """Isend + Irecv to itself for every window shape: every payload
     checksummed (check_iters == iters), the Waitall receives counted and
-    digested on the device, rx = tx at the end; then the same unchecked."""
+    digested on the device, rx = tx at the end; then the same unchecked.
+    Every expected value comes from the oracle (oracle/mpx_oracle.c: the
+    pattern's checksum, the reference's Waitall count), not from the device."""
     cap = 456131
     c, tx, rx = _self_rank(engine, cap)
     try:
         # mpx_xfer_prepare: SDMA graph chunks / the RCCL channel (a one-byte
         # exchange, once per pair; the second call is a no-op) — rx untouched
-        before = c.checksum(rx, cap)
+        rx0 = O.pattern_checksum(cap, mpx.FILL_BYTE, 0)
+        assert c.checksum(rx, cap) == rx0
         for _ in range(2):
             c.prepare(mpx.MODE_NONBLOCKING, 0, 0, 0, 600, cap)
-        assert c.checksum(rx, cap) == before
+        assert c.checksum(rx, cap) == rx0
         for n in (0, 1, 4097, 65541, cap):
-            want = c.checksum(tx, n)
+            want = O.pattern_checksum(n, mpx.FILL_SPLITMIX, SELF_KEY)
             for iters in (1, 255, 256, 257, 600):
                 t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, n, check_payload=True, expect=want,
                            timeout_ms=10000)
-                k = iters - iters // 256
+                k = O.lib().oracle_nb_waited(iters)
                 assert t.check_iters == iters and t.check_failures == 0, (n, iters)
                 assert t.recv_done == k and t.recv_digest == (k * want) & 0xFFFFFFFFFFFFFFFF, (n, iters)
                 assert c.checksum(rx, n) == want
             t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, 600, tx, rx, n, timeout_ms=10000)
-            assert t.recv_done == 600 - 2 and t.bytes == 2 * n * 600
+            assert t.recv_done == O.lib().oracle_nb_waited(600) and t.bytes == 2 * n * 600
         if engine == "rccl":
             assert t.protocol == 3
     finally:
         c.close()
+
+
+def _self_golden_cases():
+    """golden non-blocking runs of one pair (ppn 1) with the PMPI shim's
+    receive accounting of both ranks"""
+    return [c["name"] for c in O.golden()["cases"]
+            if "-x" in c["args"] and "-u" not in c["args"] and c.get("shim") and not c.get("returncode")
+            and c["ppn"] == 1]
+
+
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "rccl"])
+@pytest.mark.parametrize("name", _self_golden_cases())
+def test_self_pair_receive_digest_matches_reference(name, engine):
+    """RCCL's receive accounting pinned to the compiled reference, on one GPU.
+    In the golden run, rank 0 (group 1) receives group 0's 'a'-filled tx and
+    rank 1 receives 'b' (mpi_perf.c:244-251).  A rank paired with itself
+    whose tx holds that rank's payload receives the same bytes, so its
+    device-counted receives, bytes and digest over the run's -r runs of -i
+    iterations must equal that rank's PMPI shim numbers
+    (tests/golden/ref_runs.json).  The RCCL engine can run no other pair on a
+    one-GPU box (it refuses two ranks on one device); the kernel and SDMA
+    engines run it too."""
+    c = O.golden()["cases"][[x["name"] for x in O.golden()["cases"]].index(name)]
+    a = c["args"]
+    runs, iters = int(a[a.index("-r") + 1]), int(a[a.index("-i") + 1])
+    B = int(a[a.index("-b") + 1])
+    for rank, fill in ((0, "a"), (1, "b")):
+        ctx = mpx.Context(1, engine)
+        try:
+            tx, rx = ctx.alloc(0, B), ctx.alloc(0, B)
+            ctx.fill(tx, B, mpx.FILL_BYTE, ord(fill))
+            ctx.attach(0, 0, tx, rx, B)
+            if engine == "rccl":
+                ctx.rccl_init_all()
+            want = O.pattern_checksum(B, mpx.FILL_BYTE, ord(fill))
+            done = nbytes = dig = 0
+            for _ in range(runs):
+                t = ctx.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, B, check_payload=True, expect=want,
+                             timeout_ms=10000)
+                assert t.check_iters == iters and t.check_failures == 0
+                done += t.recv_done
+                nbytes += t.recv_done * B
+                dig = (dig + t.recv_digest) & 0xFFFFFFFFFFFFFFFF
+            ref = c["shim"][str(rank)]
+            assert [done, nbytes, dig] == [ref["recv_done"], ref["recv_bytes"], ref["recv_digest"]], (rank, engine)
+        finally:
+            ctx.close()
 
 
 @pytest.mark.parametrize("engine", ["kernel", "sdma", "rccl"])
@@ -554,7 +607,7 @@ def test_self_pair_lost_payload_fails(monkeypatch, engine):
     try:
         with pytest.raises(mpx.MpxError) as e:
             c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, 300, tx, rx, 65541, check_payload=True,
-                   expect=c.checksum(tx, 65541), timeout_ms=10000)
+                   expect=O.pattern_checksum(65541, mpx.FILL_SPLITMIX, SELF_KEY), timeout_ms=10000)
         assert e.value.status == mpx.ERR_CHECK
     finally:
         c.close()

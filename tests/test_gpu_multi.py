@@ -49,14 +49,37 @@ def ngpus() -> int:
     return mpx.device_count()
 
 
-def need(n: int, engine: str = "", distinct: bool = False):
+# What each BASELINE configuration reports on a multi-GPU node, and the
+# north_star target it is held to (BASELINE.json): named in every skip reason,
+# so a one-GPU run says what it did not measure.
+CFG = {
+    "cfg3": "BASELINE cfg3 (2 x MI355X, one pair over xGMI): per-pair unidir GB/s at 4 MiB, target >= 85 % of "
+            "the link (65.3 GB/s of one direction's 76.8; 130.6 of the 153.6 bidirectional), and the 8 B "
+            "half round trip, target < 3 us",
+    "cfg4": "BASELINE cfg4 (8 x MI355X, all 28 pairs in concurrent rounds): every pair's payloads checked, "
+            "aggregate GB/s per round reported (bench.py)",
+    "cfg5": "BASELINE cfg5 (8 x MI355X, RCCL all-pairs stress): every payload checksummed, receive digests = "
+            "the reference's, kusto_ingest-ready records",
+}
+XGMI_ONE_DIRECTION_GBPS, XGMI_BIDIR_GBPS = 76.8, 153.6
+TARGET_LINK_FRAC, TARGET_HALF_RTT_US = 0.85, 3.0
+
+
+def need(n: int, engine: str = "", distinct: bool = False, cfg: str = "cfg3"):
     if REHEARSE:
         if engine == "rccl" or distinct:
-            pytest.skip("needs distinct GPUs (one-GPU rehearsal)")
+            pytest.skip(f"needs distinct GPUs (one-GPU rehearsal); {CFG[cfg]}")
         assert os.environ.get("MPX_LL_MAX") == "8192", "rehearse with the cross-GPU LL threshold: MPX_LL_MAX=8192"
         return
     if ngpus() < n:
-        pytest.skip(f"needs {n} GPUs, {ngpus()} visible")
+        pytest.skip(f"needs {n} GPUs, {ngpus()} visible; {CFG[cfg]}")
+
+
+def report_target(record_property, name: str, value: float, unit: str, target: str, passed: bool) -> None:
+    """A north_star number with its target beside it: in the junit properties
+    and on stdout (pytest -s / -rP), whatever the verdict."""
+    record_property(name, dict(value=value, unit=unit, target=target, meets_target=passed))
+    print(f"[target] {name}: {value:.3f} {unit} (target {target}): {'MEETS' if passed else 'MISSES'}")
 
 
 # 8191 / 8192: the cross-GPU LL protocol's largest messages; 8193: bulk
@@ -119,15 +142,31 @@ def _golden_cross_cases():
     return out
 
 
-@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
 @pytest.mark.parametrize("name", _golden_cross_cases())
 def test_cfg3_receive_digest_matches_reference_across_gpus(name, engine):
     """The golden run's pairs with every rank on its own GPU (2 x ppn GPUs):
     device-counted receives, bytes and checksum digest per rank equal the
     compiled reference's (PMPI shim) numbers."""
+    _receive_digest_across_gpus(name, engine, "cfg3")
+
+
+@pytest.mark.parametrize("name", _golden_cross_cases())
+def test_cfg5_rccl_receive_digest_matches_reference_across_gpus(name):
+    """BASELINE config 5's receive check: the RCCL engine's device-counted
+    receives, bytes and digest per rank, each rank on its own GPU, equal the
+    compiled reference's ranks' (PMPI shim, tests/golden/ref_runs.json) in
+    every loop, ppn 1-4, and the non-blocking window cases — the independent
+    check of RCCL's receive accounting that one GPU cannot run (RCCL refuses
+    two ranks on one device; tests/test_gpu_engine.py pins its self-pair
+    form to the same golden digests)."""
+    _receive_digest_across_gpus(name, "rccl", "cfg5")
+
+
+def _receive_digest_across_gpus(name, engine, cfg):
     c = GOLDEN[name]
     ppn = c["ppn"]
-    need(2 * ppn, engine)
+    need(2 * ppn, engine, cfg=cfg)
     a = c["args"]
     runs = int(a[a.index("-r") + 1])
     iters = int(a[a.index("-i") + 1]) if "-i" in a else 10
@@ -172,17 +211,47 @@ def test_cfg3_cross_gpu_two_processes_ipc(tmp_path, engine):
             assert x["check_failures"] == 0 and x["check_iters"] == x["iters"], (r, x)
 
 
-def test_cfg3_cross_gpu_8B_latency_is_recorded():
+def test_cfg3_8B_half_rtt_reported_against_3us_target(record_property):
     """Ping-pong 8 B across GPUs (SURVEY §8d cfg3, 10^5 iterations): the half
-    round trip is reported (BASELINE's target: < 3 us device-initiated)."""
+    round trip, reported beside north_star's target (< 3 us device-initiated)
+    with its verdict.  The test fails only on a broken measurement (> 50 us);
+    the target's verdict is the reported field, and bench.py's
+    extras.targets carries the same check for the driver's line."""
     need(2)
     P = Pairs("kernel", 1, 64, fill="seeded", devs=cross_gpu_devs(2))
     try:
         out, errs = P.run(mpx.MODE_PINGPONG, 8, 100000, check=False)
         assert not errs, errs
-        half_rtt_us = out[0].device_s / (2 * 100000) * 1e6
-        print(f"cross-GPU 8 B half RTT {half_rtt_us:.3f} us")
+        half_rtt_us = max(out[0].device_s, out[1].device_s) / (2 * 100000) * 1e6
+        report_target(record_property, "cfg3_8B_half_rtt_us", half_rtt_us, "us", f"< {TARGET_HALF_RTT_US}",
+                      half_rtt_us < TARGET_HALF_RTT_US)
         assert 0 < half_rtt_us < 50
+    finally:
+        P.close()
+
+
+def test_cfg3_unidir_4MiB_reported_against_85pct_link_target(record_property):
+    """One pair, unidir 4 MiB x 500 (the bench's headline shape, G1 -> G0
+    over one link): per-pair GB/s from the G1 launch's device time, reported
+    beside north_star's >= 85 % of link peak, against one direction of the
+    link (76.8 GB/s, the unidirectional loop's ceiling) and against the
+    153.6 GB/s bidirectional figure BASELINE.md quotes.  Fails only on a
+    broken measurement (< 1 GB/s)."""
+    need(2)
+    n, iters = 4 << 20, 500
+    P = Pairs("kernel", 1, n, fill="seeded", devs=cross_gpu_devs(2))
+    try:
+        out, errs = P.run(mpx.MODE_UNIDIR, n, 3)                 # every payload checked first
+        assert not errs, errs
+        out, errs = P.run(mpx.MODE_UNIDIR, n, iters, check=False)
+        assert not errs, errs
+        gbps = n * iters / out[0].device_s / 1e9
+        report_target(record_property, "cfg3_unidir_4MiB_GBps", gbps, "GB/s",
+                      f">= {TARGET_LINK_FRAC} x {XGMI_ONE_DIRECTION_GBPS} (one direction)",
+                      gbps >= TARGET_LINK_FRAC * XGMI_ONE_DIRECTION_GBPS)
+        report_target(record_property, "cfg3_unidir_4MiB_frac_of_bidirectional_link", gbps / XGMI_BIDIR_GBPS, "",
+                      f">= {TARGET_LINK_FRAC} of {XGMI_BIDIR_GBPS} GB/s", gbps >= TARGET_LINK_FRAC * XGMI_BIDIR_GBPS)
+        assert gbps > 1
     finally:
         P.close()
 
@@ -218,7 +287,7 @@ def test_cfg4_all_pairs_rounds_every_gpu(tmp_path, engine):
     4 concurrent pairs = all 28 pairs), unidir 456131 B x 10 (run-hbv3's
     shape), seeded payloads, every payload checked, records for runs 1..N-1
     covering every pair once."""
-    need(2, engine)
+    need(2, engine, cfg="cfg4")
     N = _world()
     (tmp_path / "group1").write_text("vm\n")
     names = ",".join(["vm"] * (N // 2) + ["runsc"] * (N // 2))
@@ -239,7 +308,7 @@ def test_cfg5_rccl_all_pairs_stress_processes(tmp_path):
     """BASELINE config 5: one mpx_perf process per GPU (the reference's
     process model), RCCL engine, all-pairs rounds twice over, seeded payloads
     checked, and the records are what kusto_ingest.py would upload."""
-    need(2, "rccl")
+    need(2, "rccl", cfg="cfg5")
     N = _world()
     (tmp_path / "group1").write_text("vm\n")
     names = ",".join(["vm"] * (N // 2) + ["runsc"] * (N // 2))
@@ -271,7 +340,7 @@ def test_cfg5_rccl_all_pairs_stress_processes(tmp_path):
 
 def test_link_types_between_all_gpus():
     """Every pair of visible GPUs is one xGMI hop apart (full mesh)."""
-    need(2, distinct=True)
+    need(2, distinct=True, cfg="cfg4")
     for a in range(ngpus()):
         for b in range(ngpus()):
             if a != b:
@@ -282,7 +351,7 @@ def test_link_types_between_all_gpus():
 def test_concurrent_pairs_on_disjoint_links():
     """N/2 pairs at once, one per pair of GPUs (a round of cfg4), every
     payload checked in all three modes."""
-    need(4)
+    need(4, cfg="cfg4")
     N = _world()
     P = Pairs("kernel", N // 2, 4 << 20, fill="seeded", devs=cross_gpu_devs(N))
     try:

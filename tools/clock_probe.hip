@@ -24,6 +24,21 @@ __global__ void k_clock(u64* out, u64 ticks) {
     out[2 * blockIdx.x + 1] = r1 - r0;
 }
 
+// An empty kernel: its dispatch duration in a kernel trace is the fixed cost
+// of a launch (workgroup dispatch, end-of-kernel release, completion signal)
+// that every k_copy launch pays on top of its bytes.
+__global__ void k_empty(int* p) {
+    if (p && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) p[0] = 1;   // never taken
+}
+
+extern "C" int empty_kernels(int dev, int grid, int threads, int count) {
+    if (hipSetDevice(dev) != hipSuccess) return 1;
+    static hipStream_t s = nullptr;
+    if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 3;
+    for (int i = 0; i < count; ++i) hipLaunchKernelGGL(k_empty, dim3(grid), dim3(threads), 0, s, nullptr);
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : 4;
+}
+
 extern "C" int clock_probe(int dev, double ms, int wgs, double* ghz) {
     if (hipSetDevice(dev) != hipSuccess || wgs < 1) return 1;
     u64* d = nullptr;

@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIZES = [512 << 10, 1 << 20, 2 << 20, 3 << 20, 4 << 20, 8 << 20, 16 << 20]
 FORMS = ("steps", "launch")
 CALLS, COPIES, WARM = 5, 10, 2
+EMPTY, EMPTY_COUNT = ((1, 64), (128, 256), (1024, 256), (4096, 256)), 20   # (grid, lanes) of empty launches
 G = 1 << 30
 
 
@@ -40,6 +41,7 @@ def run(out_path):
 
     probe = ctypes.CDLL(os.path.join(ROOT, "tools", "libclock_probe.so"))
     probe.clock_probe.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    probe.empty_kernels.argtypes = [ctypes.c_int] * 4
 
     def clock(wgs):
         g = ctypes.c_double(0)
@@ -64,6 +66,9 @@ def run(out_path):
                     c.copy(0, dst, src, G, 10)
                 schedule.append(dict(state=state, what="headline", dispatches=200))
             emit(dict(state=state, clock_ghz_1wg=clock(1), clock_ghz_per_cu=clock(256)))
+            for grid, threads in EMPTY:
+                probe.empty_kernels(0, grid, threads, EMPTY_COUNT)
+            schedule.append(dict(state=state, what="empty"))
             for n in SIZES:
                 for form in FORMS:
                     os.environ["MPX_COPY_STEPS_MAX"] = str(16 << 20) if form == "steps" else "0"
@@ -86,13 +91,24 @@ def run(out_path):
 def summary(lab_path, trace_path):
     lines = [json.loads(x) for x in open(lab_path)]
     schedule = next(x["schedule"] for x in lines if "schedule" in x)
-    rows = [r for r in csv.DictReader(open(trace_path)) if "k_copy" in r["Kernel_Name"]]
-    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    every = sorted(csv.DictReader(open(trace_path)), key=lambda r: int(r["Dispatch_Id"]))
+    rows = [r for r in every if "k_copy" in r["Kernel_Name"]]
+    empty = [r for r in every if "k_empty" in r["Kernel_Name"]]
     k = 0
     res = []
     for item in schedule:
         if item.get("what") == "headline":
             k += item["dispatches"]
+            continue
+        if item.get("what") == "empty":
+            mine, empty = empty[:len(EMPTY) * EMPTY_COUNT], empty[len(EMPTY) * EMPTY_COUNT:]
+            for j, (grid, threads) in enumerate(EMPTY):
+                d = mine[j * EMPTY_COUNT:(j + 1) * EMPTY_COUNT]
+                dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in d]
+                gap = [(int(d[i + 1]["Start_Timestamp"]) - int(d[i]["End_Timestamp"])) / 1e3 for i in range(len(d) - 1)]
+                res.append(dict(state=item["state"], empty_kernel=dict(grid=grid, lanes=threads),
+                                kernel_us_median=round(statistics.median(dur), 3),
+                                gap_us_median=round(statistics.median(gap), 3)))
             continue
         steps = item["path"] == "copy_steps"
         calls = []
