@@ -12,6 +12,7 @@
 
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <map>
 #include <mutex>
@@ -358,12 +359,12 @@ bool plain_streams() {
 // of a context freed before its streams are destroyed, a long-lived process
 // that creates and finalizes contexts one after another stalled in a later
 // context (the -m gpu suite: profiles/r02_stream_destroy_suite_hang.txt,
-// r02_stream_pool_ab.txt) unless the destroy waits ~50 ms after the drain —
+// r02_stream_pool_ab.txt) when each destroy followed its drain directly —
 // the runtime still finishes a drained stream's last commands on its HSA
-// event thread (the exit stall below, same race).  A device-wide
-// hipDeviceSynchronize before each destroy, without the delay, does not
-// prevent it: the engine tests stalled after 161 passed, inside the next
-// context's first fill (profiles/r02_stream_destroy_devsync.txt).  So rank streams are
+// event thread (the exit stall below, same race; callback_fence closes it).
+// A device-wide hipDeviceSynchronize before each destroy does not: the
+// engine tests stalled after 161 passed, inside the next context's first
+// fill (profiles/r02_stream_destroy_devsync.txt).  Rank streams are
 // process-lifetime objects, like the runtime's own queues: mpx_finalize
 // drains them, frees every allocation of the context, and returns them to a
 // per-device pool that later contexts reuse; an exit handler destroys the
@@ -388,36 +389,62 @@ StreamPool& pool() {
 
 void destroy_stream_pool();
 
-void release_rank_stream(int dev, hipStream_t s) {
-    // MPX_STREAM_POOL=0: every mpx_finalize destroys its rank streams,
-    // MPX_STREAM_POOL_DELAY_MS (default 50) after their drain — the same
-    // wait as at exit (destroy_stream_pool).  With it the engine tests pass
-    // with a destroy per finalize; without it they stalled inside a later
-    // mpx_finalize (profiles/r02_stream_pool_ab.txt).  Opt-in: the pool never
-    // destroys a stream while the process runs.
-    static const bool no_pool = [] {
-        const char* v = getenv("MPX_STREAM_POOL");
-        return v && atoi(v) == 0;
-    }();
-    static const int delay_ms = [] {
-        const char* v = getenv("MPX_STREAM_POOL_DELAY_MS");
-        return v ? atoi(v) : 50;
-    }();
-    if (plain_streams()) {
-        (void)hipStreamDestroy(s);
-        return;
+void fence_cb(void* p) { static_cast<std::atomic<int>*>(p)->fetch_add(1, std::memory_order_release); }
+
+// Before rank streams are destroyed.  hipStreamSynchronize returns when a
+// stream's commands are complete, but the runtime's HSA event thread may
+// still be inside the completion callback of the last one; a stream
+// destroyed under that callback leaves the thread waiting forever, and the
+// process stalls at exit (profiles/r02_exit_stall.txt) or in a later
+// context.  So two host functions go onto each stream as its last commands,
+// and the destroy waits until the SECOND has run: the event thread runs a
+// stream's callbacks in order, so by then every callback before it,
+// the first host function included, has returned.  The stream is drained
+// once more (its last command: the second host function) and then destroyed.
+// Minimal repro without libmpx (tools/exit_stall_repro.hip,
+// tools/gpu_exit_stall.sh; profiles/r03_exit_stall_repro.jsonl): two
+// CU-masked streams, 300 x {64 KiB copy, one-lane kernel} each, drained,
+// destroyed, exit — 8 of 10 processes stalled at exit with the destroy
+// right after the drain, 0 of 10 with this fence (0 of 10 with a 50 ms
+// sleep, round 2's workaround, now removed).  The wait for the callbacks is
+// bounded (10 s) only so that a runtime that never runs them cannot hang
+// the caller; the order, not the time, is what the fence relies on.
+void callback_fence(const std::vector<std::pair<int, hipStream_t>>& ss) {
+    // heap-held counters: leaked if the bound expires, so a late callback
+    // never writes freed memory
+    std::atomic<int>* cnt = new std::atomic<int>[ss.size() ? ss.size() : 1];
+    std::vector<bool> armed(ss.size(), false);
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (size_t i = 0; i < ss.size(); ++i) {
+        cnt[i].store(0);
+        (void)hipSetDevice(ss[i].first);
+        armed[i] = hipLaunchHostFunc(ss[i].second, fence_cb, &cnt[i]) == hipSuccess &&
+                   hipLaunchHostFunc(ss[i].second, fence_cb, &cnt[i]) == hipSuccess;
+        (void)hipGetLastError();
     }
-    if (no_pool) {
-        {
-            std::lock_guard<std::mutex> lk(pool().mu);
-            auto& all = pool().all;
-            for (size_t i = 0; i < all.size(); ++i)
-                if (all[i].second == s) {
-                    all.erase(all.begin() + (long)i);
-                    break;
-                }
-        }
-        if (delay_ms > 0) usleep((useconds_t)delay_ms * 1000u);
+    const double t_end = now_s() + 10.0;
+    bool done = true;
+    for (size_t i = 0; i < ss.size(); ++i) {
+        while (armed[i] && cnt[i].load(std::memory_order_acquire) < 2 && now_s() < t_end) usleep(50);
+        done &= !armed[i] || cnt[i].load(std::memory_order_acquire) >= 2;
+        (void)hipSetDevice(ss[i].first);
+        (void)hipStreamSynchronize(ss[i].second);
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (done) delete[] cnt;
+    else if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] callback fence: host functions did not run in 10 s\n");
+}
+
+// A rank stream goes back to the pool; it is never destroyed while the
+// process runs.  Round 2's opt-in destroy per finalize (MPX_STREAM_POOL=0)
+// is gone: with callback_fence in place of its 50 ms wait the engine tests
+// still stalled inside a later mpx_finalize (profiles/r03_pytest_nopool.log),
+// as they did after a device-wide synchronize (r02_stream_destroy_devsync.txt)
+// — destroying a CU-masked stream mid-process is unsafe on this runtime
+// whatever ordering precedes it, so the pool is the design, not a default.
+void release_rank_stream(int dev, hipStream_t s) {
+    if (plain_streams()) {
         (void)hipStreamDestroy(s);
         return;
     }
@@ -462,31 +489,20 @@ void destroy_stream_pool() {
     // the runtime.  libmpx's own hosts never get here on a failure: MPX_CHECK
     // flushes stdio and _exits (host/mpx_perf.c, integration/mpx_binding.c).
     if (p.live_contexts != 0 || p.all.empty()) return;
-    // The runtime finishes a drained stream's last commands on its HSA event
-    // thread (completion callbacks) slightly after hipStreamSynchronize
-    // returns.  Destroying the stream under a callback still in flight left
-    // the runtime's own exit teardown (HIP's static destructors, in
-    // __cxa_finalize) waiting forever on that thread: mpx_perf -e sdma -x 1
-    // -c 1, two ranks on GPU 0, stalled after its last line in 2 of 4 suite
-    // runs and in the first attempt of tools/gpu_exit_hang.sh (all-thread
-    // stacks: profiles/r02_exit_stall.txt).  With 50 ms between the drain
-    // and the destroys, 0 of 6 attempts stalled; with the streams left to the
-    // runtime, 0 of 6 (but then the runtime destroys them after a profiler's
-    // exit handler, which crashed under rocprofv3 in round 1).
-    // MPX_POOL_EXIT=keep leaves them to the runtime; MPX_POOL_EXIT_DELAY_MS
-    // sets the wait (A/B knobs).
+    // Destroyed after callback_fence: a stream destroyed under a completion
+    // callback still in flight left the runtime's own exit teardown (HIP's
+    // static destructors, in __cxa_finalize) waiting forever on the event
+    // thread (mpx_perf -e sdma -x 1 -c 1, two ranks on GPU 0: stalled after
+    // its last line in 2 of 4 suite runs; all-thread stacks in
+    // profiles/r02_exit_stall.txt).  Left to the runtime instead, they are
+    // destroyed after a profiler's exit handler, which crashed under
+    // rocprofv3 in round 1.  MPX_POOL_EXIT=keep leaves them (A/B knob).
     const char* mode = getenv("MPX_POOL_EXIT");
     if (mode && !strcmp(mode, "keep")) return;
-    const char* delay = getenv("MPX_POOL_EXIT_DELAY_MS");
-    const int delay_ms = (delay && *delay) ? atoi(delay) : 50;
     if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] exit: destroying %zu pooled rank streams\n", p.all.size());
     int prev = -1;
     (void)hipGetDevice(&prev);
-    for (auto& ds : p.all) {
-        (void)hipSetDevice(ds.first);
-        (void)hipStreamSynchronize(ds.second);
-    }
-    if (delay_ms > 0) usleep((useconds_t)delay_ms * 1000u);
+    callback_fence(p.all);
     for (auto& ds : p.all) {
         (void)hipSetDevice(ds.first);
         (void)hipStreamDestroy(ds.second);
@@ -1090,15 +1106,20 @@ int mpx_finalize(mpx_ctx* ctx) {
     // Teardown order matters: every stream is drained and every allocation
     // freed, then the rank streams go back to the process pool (the teardown
     // rule above create_rank_stream).
+    // Every stream of the context, rank and utility streams alike, is
+    // drained through callback_fence: no completion callback of any of them
+    // is still running when their memory is freed and the utility streams
+    // are destroyed (a utility stream destroyed right after its drain stalled
+    // mpx_perf at exit once the rank streams were fenced: r03_exit_hang).
+    std::vector<std::pair<int, hipStream_t>> ss;
     for (int i = 0; i < MPX_MAX_RANKS; ++i) {
         Rank& rk = ctx->r[i];
         if (rk.comm) (void)ncclCommDestroy(rk.comm);
         rk.comm = nullptr;
-        if (rk.local && rk.stream) {
-            DeviceGuard g(rk.dev);
-            (void)hipStreamSynchronize(rk.stream);
-        }
+        if (rk.local && rk.stream) ss.emplace_back(rk.dev, rk.stream);
     }
+    for (auto& kv : ctx->dev_stream) ss.emplace_back(kv.first, kv.second);
+    callback_fence(ss);
     DBG("finalize: streams drained\n");
     for (int i = 0; i < MPX_MAX_RANKS; ++i) {
         for (auto& kv : ctx->r[i].sdma_graphs) (void)hipGraphExecDestroy(kv.second);
