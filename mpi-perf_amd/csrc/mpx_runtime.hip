@@ -359,22 +359,19 @@ bool plain_streams() {
 // of a context freed before its streams are destroyed, a long-lived process
 // that creates and finalizes contexts one after another stalled in a later
 // context (the -m gpu suite: profiles/r02_stream_destroy_suite_hang.txt,
-// r02_stream_pool_ab.txt) when each destroy followed its drain directly —
-// the runtime still finishes a drained stream's last commands on its HSA
-// event thread (the exit stall below, same race; callback_fence closes it).
-// A device-wide hipDeviceSynchronize before each destroy does not: the
-// engine tests stalled after 161 passed, inside the next context's first
-// fill (profiles/r02_stream_destroy_devsync.txt).  Rank streams are
+// r02_stream_pool_ab.txt) when each destroy followed its drain directly,
+// and still did after a device-wide hipDeviceSynchronize
+// (profiles/r02_stream_destroy_devsync.txt) or after callback_fence
+// (profiles/r03_pytest_nopool.log).  Rank streams are therefore
 // process-lifetime objects, like the runtime's own queues: mpx_finalize
-// drains them, frees every allocation of the context, and returns them to a
-// per-device pool that later contexts reuse; an exit handler destroys the
-// pool when no context is alive (all memory they touched is freed by then —
-// the safe order).  No HIP call may run later than that at exit: under
-// rocprofv3 the tool finalizes in its own exit handler, and a HIP call after
-// it (the runtime's exit teardown of leaked streams in round 1, or this pool
-// destroyed from a library destructor) ends in SIGSEGV in __cxa_finalize
-// (profiles/r02_prof_n2_exit.txt).  The handler is registered with atexit()
-// when the first rank stream is created, i.e. after the tool's, so it runs
+// drains them (callback_fence), frees every allocation of the context, and
+// returns them to a per-device pool that later contexts reuse.  At exit they
+// are left to the runtime's teardown (destroy_stream_pool below): every
+// allocation their kernels touched is freed by then — the safe order.  A HIP
+// call from a library destructor after a profiler's exit handler ends in
+// SIGSEGV in __cxa_finalize (profiles/r02_prof_n2_exit.txt), so the exit
+// handler that can destroy them (MPX_POOL_EXIT A/B modes) is registered with
+// atexit() when the first rank stream is created, after the tool's, and runs
 // before it.
 struct StreamPool {
     std::mutex mu;
@@ -478,31 +475,49 @@ int create_rank_stream(int dev, hipStream_t* s) {
     return MPX_OK;
 }
 
-// exit handler (registered at the first rank stream, see above)
+// exit handler (registered at the first rank stream, see above).
+// By default the pooled rank streams are NOT destroyed: every context has
+// been finalized by then (each drained its streams through callback_fence
+// and freed all it allocated — the safe order), and the runtime's own exit
+// teardown releases the streams and their queues.  Measured (round 3):
+//  * left to the runtime: mpx_perf in processes mode (two processes on GPU
+//    0, IPC-mapped) 4 of 4 clean exits; exit 0 under rocprofv3 for bench.py
+//    and mpx_perf (profiles/r03_exit_order_ab.txt) — round 1's SIGSEGV in
+//    __cxa_finalize came from streams leaked with memory still allocated;
+//  * destroyed here after callback_fence: 2 of 4 clean in processes mode —
+//    the event thread stalls inside a completion callback that no fence of
+//    ours orders (it is not one of our streams' commands; a device-wide
+//    synchronize before the destroy made it 0 of 4);
+//  * destroyed 50 ms after the drain (round 2): 4 of 4, but only time orders it.
+// MPX_POOL_EXIT=destroy | devsync | sleep selects those orders (A/B).
 void destroy_stream_pool() {
     StreamPool& p = pool();
     std::lock_guard<std::mutex> lk(p.mu);
-    // A context still alive at exit owns memory its streams' kernels touched:
-    // destroying the streams before that memory is freed is the order that
-    // hangs the runtime's exit teardown (above), and freeing it here could pull
-    // it from under another thread still inside a call.  So they are left to
-    // the runtime.  libmpx's own hosts never get here on a failure: MPX_CHECK
-    // flushes stdio and _exits (host/mpx_perf.c, integration/mpx_binding.c).
-    if (p.live_contexts != 0 || p.all.empty()) return;
-    // Destroyed after callback_fence: a stream destroyed under a completion
-    // callback still in flight left the runtime's own exit teardown (HIP's
-    // static destructors, in __cxa_finalize) waiting forever on the event
-    // thread (mpx_perf -e sdma -x 1 -c 1, two ranks on GPU 0: stalled after
-    // its last line in 2 of 4 suite runs; all-thread stacks in
-    // profiles/r02_exit_stall.txt).  Left to the runtime instead, they are
-    // destroyed after a profiler's exit handler, which crashed under
-    // rocprofv3 in round 1.  MPX_POOL_EXIT=keep leaves them (A/B knob).
+    // A context still alive at exit owns memory its streams' kernels touched
+    // (see the teardown rule above); libmpx's own hosts never get here on a
+    // failure: MPX_CHECK flushes stdio and _exits (host/mpx_perf.c,
+    // integration/mpx_binding.c).
     const char* mode = getenv("MPX_POOL_EXIT");
-    if (mode && !strcmp(mode, "keep")) return;
+    if (!mode || !*mode || !strcmp(mode, "keep") || p.live_contexts != 0 || p.all.empty()) return;
     if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] exit: destroying %zu pooled rank streams\n", p.all.size());
     int prev = -1;
     (void)hipGetDevice(&prev);
-    callback_fence(p.all);
+    if (!strcmp(mode, "sleep")) {
+        for (auto& ds : p.all) {
+            (void)hipSetDevice(ds.first);
+            (void)hipStreamSynchronize(ds.second);
+        }
+        usleep(50000);
+    } else {
+        callback_fence(p.all);
+        if (!strcmp(mode, "devsync")) {
+            for (auto& ds : p.all) {
+                (void)hipSetDevice(ds.first);
+                (void)hipDeviceSynchronize();
+            }
+            callback_fence(p.all);
+        }
+    }
     for (auto& ds : p.all) {
         (void)hipSetDevice(ds.first);
         (void)hipStreamDestroy(ds.second);

@@ -9,7 +9,7 @@ echo "node-0" > group1
 N=${N:-6}
 for a in $(seq 1 $N); do
     rm -rf logs
-    MPX_DEBUG=1 MPX_POOL_EXIT=${MPX_POOL_EXIT:-} MPX_POOL_EXIT_DELAY_MS=${MPX_POOL_EXIT_DELAY_MS:-} MPX_PROCESSOR_NAMES= MPX_HOSTNAME=node ../../mpi-perf_amd/bin/mpx_perf -w 2 -g 0,0 -e ${ENGINE:-sdma} \
+    MPX_DEBUG=1 MPX_POOL_EXIT=${MPX_POOL_EXIT:-} MPX_PROCESSOR_NAMES= MPX_HOSTNAME=node ../../mpi-perf_amd/bin/mpx_perf -w 2 -g 0,0 -e ${ENGINE:-sdma} \
         -f group1 -n 1 -p 1 -r 3 -i 300 -b 65536 -l logs -x 1 -c 1 -t 5000 > out_$a.txt 2> err_$a.txt &
     pid=$!
     t=0
