@@ -314,8 +314,9 @@ int skip_push_knob() {
 }
 
 // test knob (MPX_TEST_LAG_WG="rank:wg:us"): in non-blocking check mode,
-// workgroup wg of `rank` stalls `us` microseconds before it checks the call's
-// last receive, so that rank's call ends long after its peer's; read per call
+// workgroup wg of `rank` (wg < 0 counts from the last) stalls `us`
+// microseconds before it checks the call's last receive, so that rank's call
+// ends long after its peer's; read per call
 void lag_knob(int my_rank, int* wg, u64* ticks) {
     *wg = 0;
     *ticks = 0;
@@ -617,6 +618,7 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.slots = link_slots(me, peer, len);
     a.skip_push = skip_push_knob();
     lag_knob(my_rank, &a.lag_wg, &a.lag_ticks);
+    if (a.lag_wg < 0) a.lag_wg += a.nwg;   // -1: the last pushing workgroup
     if (a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!me.ring || !peer.ring))
         return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
 

@@ -35,12 +35,14 @@ def wait_for(d, name):
 def main():
     d, rank, engine, scenario = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
     peer = 1 - rank
+    # MPX_ORDER_CROSS=1: rank r on GPU r (the pair spans GPUs, bytes over xGMI)
+    dev = rank if os.environ.get("MPX_ORDER_CROSS") and not os.environ.get("MPX_MULTI_REHEARSE") else 0
     c = mpx.Context(2, engine)
-    tx, rx, scratch = c.alloc(0, O.CAP), c.alloc(0, O.CAP), c.alloc(0, O.CAP)
+    tx, rx, scratch = c.alloc(dev, O.CAP), c.alloc(dev, O.CAP), c.alloc(dev, O.CAP)
     sums = O.pattern_sums(c, scratch, rank, peer)
     c.fill(tx, O.CAP, mpx.FILL_SPLITMIX, O.key(rank, peer, 0))
     c.fill(rx, O.CAP, mpx.FILL_BYTE, 0)
-    c.attach(rank, 0, tx, rx, O.CAP)
+    c.attach(rank, dev, tx, rx, O.CAP)
     publish(d, f"desc_{rank}.bin", c.export(rank))
     publish(d, f"sums_{rank}.json", json.dumps(sums).encode())
     c.import_rank(peer, wait_for(d, f"desc_{peer}.bin"))

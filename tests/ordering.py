@@ -29,9 +29,10 @@ CAP = 1 << 20
 LAG_N1, LAG_N2, LAG_NWG2 = CAP, CAP - 4083, 8
 LAG_ITERS = 300
 LAG_US = 300_000
-# rank 1's last workgroup of call 1 (1 MiB within one GPU: 64 workgroups of
-# 16 KiB, bulk_nwg); call 2's workgroup 7 covers its bytes
-LAG_WG = 63
+# rank 1's last workgroup of call 1 (-1: counted from the last; 1 MiB is 64
+# workgroups of 16 KiB within one GPU, 32 of 32 KiB across GPUs, bulk_nwg);
+# call 2's last workgroup (7 of 8) covers its bytes
+LAG_WG = -1
 RACE_DELAY_S = 0.3
 SIZES = (1, 1024, 4097, 65536 + 13, 262144 + 13, LAG_N1, LAG_N2)
 

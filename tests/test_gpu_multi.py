@@ -211,6 +211,34 @@ def test_cfg3_cross_gpu_two_processes_ipc(tmp_path, engine):
             assert x["check_failures"] == 0 and x["check_iters"] == x["iters"], (r, x)
 
 
+@pytest.mark.parametrize("mode", ["pingpong", "unidir", "nonblocking"])
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+def test_cfg3_rx_read_between_calls_across_gpus(engine, mode):
+    """Matched-receive order across xGMI (tests/test_gpu_ordering.py's race
+    scenario with rank r on GPU r): rank 1 reads rx on the host between two
+    calls while rank 0 races into the second with a new payload; rx must
+    still hold call 1's last payload, and call 2's afterwards."""
+    need(2, engine)
+    import ordering as OR
+    import test_gpu_ordering as T
+    m = {"pingpong": mpx.MODE_PINGPONG, "unidir": mpx.MODE_UNIDIR, "nonblocking": mpx.MODE_NONBLOCKING}[mode]
+    for n in (262144 + 13, 1024):
+        it = 300 if m == mpx.MODE_NONBLOCKING else 20
+        out = T.run_threads(lambda c, r, tx, rx, s: OR.race(c, r, tx, rx, s, m, True, n, it), engine,
+                            devs=cross_gpu_devs(2))
+        T.assert_race_ok(out)
+
+
+def test_cfg3_lagging_workgroup_layout_change_across_gpus(tmp_path):
+    """The non-blocking check-mode regression (GPUTEST_r02) across xGMI, two
+    processes, rank r on GPU r: one receiver workgroup late to check call
+    1's last receive, call 2 with another length and push width."""
+    need(2)
+    import ordering as OR
+    import test_gpu_ordering as T
+    T.assert_lag_ok(T.run_processes(tmp_path, "kernel", ["lag"], OR.lag_env(), cross=True))
+
+
 def test_cfg3_8B_half_rtt_reported_against_3us_target(record_property):
     """Ping-pong 8 B across GPUs (SURVEY §8d cfg3, 10^5 iterations): the half
     round trip, reported beside north_star's target (< 3 us device-initiated)

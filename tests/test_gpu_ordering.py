@@ -38,17 +38,19 @@ MODES = {"pingpong": mpx.MODE_PINGPONG, "unidir": mpx.MODE_UNIDIR, "nonblocking"
 RACE_CASES = [(262144 + 13, 20), (1024, 20)]
 
 
-def run_threads(fn, engine="kernel"):
+def run_threads(fn, engine="kernel", devs=(0, 0)):
+    """two ranks of one context on host threads; rank r on GPU devs[r]"""
     c = mpx.Context(2, engine)
     try:
         bufs, sums = [], []
-        scratch = c.alloc(0, O.CAP)
         for r in range(2):
-            tx, rx = c.alloc(0, O.CAP), c.alloc(0, O.CAP)
+            d = devs[r]
+            scratch = c.alloc(d, O.CAP)
+            tx, rx = c.alloc(d, O.CAP), c.alloc(d, O.CAP)
             sums.append(O.pattern_sums(c, scratch, r, 1 - r))
             c.fill(tx, O.CAP, mpx.FILL_SPLITMIX, O.key(r, 1 - r, 0))
             c.fill(rx, O.CAP, mpx.FILL_BYTE, 0)
-            c.attach(r, 0, tx, rx, O.CAP)
+            c.attach(r, d, tx, rx, O.CAP)
             bufs.append((tx, rx))
         out, errs = {}, {}
 
@@ -69,8 +71,11 @@ def run_threads(fn, engine="kernel"):
         c.close()
 
 
-def run_processes(tmp_path, engine, args, env_extra=None):
+def run_processes(tmp_path, engine, args, env_extra=None, cross=False):
+    """two processes, IPC-mapped; cross: rank r on GPU r (MPX_ORDER_CROSS)"""
     env = dict(os.environ, **(env_extra or {}))
+    if cross:
+        env["MPX_ORDER_CROSS"] = "1"
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "order_worker.py"), str(tmp_path), str(r), engine,
                                *[str(a) for a in args]], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                               env=env) for r in (0, 1)]
@@ -92,7 +97,7 @@ def assert_lag_ok(out):
             assert x["ok"], (r, call, x)
             assert x["check_iters"] == O.LAG_ITERS, (r, call, x)
         assert out[r]["call2"]["nwg"] == O.LAG_NWG2, out[r]
-    assert out[0]["call1"]["nwg"] > O.LAG_WG, out   # the lagging workgroup existed in call 1
+    assert out[0]["call1"]["nwg"] > O.LAG_NWG2, out   # call 2 narrows the push: every chunk boundary moves
 
 
 def assert_race_ok(out):
