@@ -20,7 +20,8 @@ constexpr int kStageMaxBytes = 60 << 10; // LDS-staged tx chunk per workgroup, m
                                          // (under a 64 KiB per-workgroup LDS limit)
 
 // Protocol ids reported in mpx_timing.protocol
-enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4, kProtoCopySteps = 5 };
+enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4, kProtoCopySteps = 5,
+             kProtoCopyPipe = 6 };
 
 // One rank's receive mailbox, in that rank's HBM (uncached / fine-grained so a
 // poll sees stores that arrive over xGMI).  Written ONLY by the peers, polled
@@ -173,6 +174,11 @@ constexpr int kCopyStepsMaxGrid = 1024;   // 4 workgroups per CU: always co-resi
 constexpr size_t kCopyStepsDefaultMax = (size_t)1 << 20;
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
                              int* grid_out);
+// all `iters` copies in one k_copy_pipe launch (copy s+1's loads in flight
+// across copy s's grid barrier, a dedicated barrier wave); *bar must be 0
+constexpr int kCopyPipeMaxGrid = 768;     // 320-lane workgroups, 3 per CU: resident
+hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
+                            int* grid_out);
 hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s);
 hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s);
 hipError_t launch_signal(u64* flag, const u64* base, u64 value, hipStream_t s);

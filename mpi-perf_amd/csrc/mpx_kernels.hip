@@ -210,6 +210,120 @@ __global__ __launch_bounds__(T) void k_copy_steps(const v4u* __restrict__ src, v
 }
 
 // ---------------------------------------------------------------------------
+// k_copy_pipe: the same `iters` back-to-back copies in ONE launch, for the
+// sizes where k_copy_steps pays three memory round trips per copy (loads,
+// then the stores' completion — __syncthreads drains them —, then the grid
+// barrier's atomic and poll; profiles/r03_copy_cliff_*).  Here a copy's step
+// costs about one:
+//  * four "copy" waves own UPL 16-B units per lane; copy s+1's loads are
+//    issued BEFORE copy s's stores (src is read-only while the copies run,
+//    and dst is written only by the stores), so they are in flight during
+//    copy s's grid barrier; two register sets, unrolled by two, no moves;
+//  * a fifth wave runs the grid barrier: its vector-memory counter holds
+//    only the barrier's atomic and poll, so waiting for the poll never waits
+//    for the copy waves' stores.  Workgroup barriers are plain s_barrier
+//    (no fence: nothing drains); the copy waves wait only for their own
+//    loads of the next copy (vmcnt counts in issue order, and those loads
+//    are older than this copy's stores).
+// Copy s+1's stores are issued only after every workgroup has issued copy
+// s's stores (the grid barrier orders issue); the kernel's end makes every
+// store visible, as a launch per copy does.
+// ---------------------------------------------------------------------------
+constexpr int kPipeCopyWaves = 4;
+constexpr int kPipeThreads = (kPipeCopyWaves + 1) * 64;   // + the barrier wave
+constexpr int kAuxNt = 2;                                 // buffer op: nt (streaming)
+
+
+__device__ __forceinline__ void wg_barrier_nofence() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS (s_stop) before the barrier
+    __builtin_amdgcn_s_barrier();
+}
+
+// Branch-free copy-wave code: every unit is a buffer op whose resource ends at
+// n16 units (out-of-range loads return 0, out-of-range stores are dropped),
+// so the compiler can count each wait exactly (a guarded unit made it wait
+// for every outstanding load, the next copy's included).  The < 16 tail bytes
+// go the same way through a resource that is empty except in workgroup 0's
+// first wave.
+template <int UPL>
+// (no __restrict__ on src: with it the optimiser may assume src's bytes never
+// change during the kernel and keep the first copy's values for every copy)
+__global__ __launch_bounds__(kPipeThreads) void k_copy_pipe(const v4u* src, v4u* dst,
+                                                          size_t n16, unsigned tail, int iters, u64* bar) {
+    __shared__ int s_stop;
+    if (threadIdx.x >= kPipeCopyWaves * 64) {
+        // the barrier wave: one grid barrier per copy boundary
+        for (int s = 0; s + 1 < iters; ++s) {
+            wg_barrier_nofence();                      // every copy wave issued copy s's stores
+            if (threadIdx.x == kPipeCopyWaves * 64) {
+                s_stop = 0;
+                __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const u64 want = (u64)gridDim.x * (u64)(s + 1);
+                const u64 t0 = now_ticks();
+                u64 spins = 0;
+                while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                    if ((++spins & 255) == 0 && now_ticks() - t0 > 100000000ull) {
+                        // 1 s: a workgroup never arrived (bar[1] -> mpx_copy's fallback)
+                        __hip_atomic_store(&bar[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        s_stop = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            wg_barrier_nofence();
+            if (s_stop) return;
+        }
+        return;
+    }
+    const unsigned stride16 = gridDim.x * (kPipeCopyWaves * 64) * 16u;     // bytes between a lane's units
+    const unsigned first16 = (blockIdx.x * (kPipeCopyWaves * 64) + threadIdx.x) * 16u;
+    const unsigned body = (unsigned)(n16 * 16);
+    const __amdgpu_buffer_rsrc_t rs = rsrc(src, body), rd = rsrc(dst, body);
+    // wave-uniform, made scalar so the tail resources live in SGPRs
+    const unsigned tb = __builtin_amdgcn_readfirstlane((blockIdx.x == 0 && threadIdx.x < 64) ? tail : 0u);
+    const __amdgpu_buffer_rsrc_t ts = rsrc(reinterpret_cast<const unsigned char*>(src) + body, tb);
+    const __amdgpu_buffer_rsrc_t td = rsrc(reinterpret_cast<unsigned char*>(dst) + body, tb);
+    v4u a[UPL], b[UPL];
+    unsigned char ta, tb8;
+    auto load = [&](v4u (&r)[UPL], unsigned char& t) {
+        // a compiler barrier: the buffer-load builtin is a plain memory read to
+        // the optimiser, which would otherwise reuse the previous copy's values
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < UPL; ++u)
+            r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, first16 + u * stride16, 0, kAuxNt);
+        t = __builtin_amdgcn_raw_buffer_load_b8(ts, threadIdx.x, 0, 0);
+    };
+    auto store = [&](v4u (&r)[UPL], unsigned char t) {
+#pragma unroll
+        for (int u = 0; u < UPL; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(r[u], rd, first16 + u * stride16, 0, kAuxNt);
+        __builtin_amdgcn_raw_buffer_store_b8(t, td, threadIdx.x, 0, 0);
+    };
+    // both workgroup barriers of a grid barrier; false: the barrier gave up
+    auto grid_barrier = [&]() -> bool {
+        wg_barrier_nofence();
+        wg_barrier_nofence();
+        return !s_stop;
+    };
+    // copy s+1's loads are issued before copy s's stores (src is read-only
+    // while the copies run), so they fly during copy s's grid barrier
+    load(a, ta);
+    for (int s = 0;;) {
+        if (s + 1 == iters) { store(a, ta); break; }
+        load(b, tb8);
+        store(a, ta);
+        if (!grid_barrier()) break;
+        if (++s + 1 == iters) { store(b, tb8); break; }
+        load(a, ta);
+        store(b, tb8);
+        if (!grid_barrier()) break;
+        ++s;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_fill
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_fill(unsigned char* p, size_t n, int pattern, u64 arg) {
@@ -1052,6 +1166,36 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
     hipLaunchKernelGGL(k, dim3((unsigned)(one_xcd ? grid * 8 : grid)), dim3((unsigned)threads), 0, s,
                        reinterpret_cast<const v4u*>(src), reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters,
                        bar, drain, one_xcd);
+    return hipGetLastError();
+}
+
+// All `iters` copies in one k_copy_pipe launch: UPL units per lane chosen so
+// the grid (<= kCopyPipeMaxGrid workgroups of 320 lanes, all resident) covers
+// n; returns hipErrorInvalidValue when n is too large for a resident grid.
+hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
+                            int* grid_out) {
+    const size_t n16 = n / 16;
+    const size_t lanes = (size_t)kPipeCopyWaves * 64;
+    // resident grid: 5-wave workgroups, as many per CU as the VGPRs allow
+    // (UPL 16: 208 VGPRs, one per CU; UPL 8: 112, three; UPL <= 4: six)
+    auto cap_of = [](int u) -> size_t { return u >= 16 ? 256 : u >= 8 ? 512 : (size_t)kCopyPipeMaxGrid; };
+    int upl = 4;
+    if (const char* v = getenv("MPX_COPY_PIPE_UPL")) upl = atoi(v);   // A/B knob, read per call
+    upl = upl <= 1 ? 1 : upl <= 2 ? 2 : upl <= 4 ? 4 : upl <= 8 ? 8 : 16;
+    size_t grid = (n16 + lanes * upl - 1) / (lanes * upl);
+    while (grid > cap_of(upl) && upl < 16) {
+        upl *= 2;
+        grid = (n16 + lanes * upl - 1) / (lanes * upl);
+    }
+    if (grid > cap_of(upl) || n >= ((size_t)1 << 32)) return hipErrorInvalidValue;
+    if (grid < 1) grid = 1;
+    if (grid_out) *grid_out = (int)grid;
+    void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*) =
+        upl <= 1 ? k_copy_pipe<1> : upl <= 2 ? k_copy_pipe<2> : upl <= 4 ? k_copy_pipe<4>
+        : upl <= 8 ? k_copy_pipe<8> : k_copy_pipe<16>;
+    (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kPipeThreads), 0, s, reinterpret_cast<const v4u*>(src),
+                       reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters, bar);
     return hipGetLastError();
 }
 

@@ -298,6 +298,13 @@ size_t copy_steps_max() {
     return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyStepsDefaultMax;
 }
 
+// Largest copy whose iterations run in one k_copy_pipe launch
+// (MPX_COPY_PIPE_MAX bytes, read per call; 0 = never)
+size_t copy_pipe_max() {
+    const char* v = getenv("MPX_COPY_PIPE_MAX");
+    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)0;
+}
+
 // the receives the reference's non-blocking loop completes (Waitall) for
 // `iters` iterations: slot 255 of each full window is never waited for
 // (mpi_perf.c:95-124)
@@ -1307,23 +1314,27 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     int grid = 0;
     // copies of <= copy_steps_max() bytes run all iterations in one launch
     // (k_copy_steps: dispatch-bound sizes); larger ones one k_copy launch each
-    bool steps = n && iters > 1 && n <= copy_steps_max();
+    const bool pipe = n && iters > 1 && n <= copy_pipe_max();
+    bool steps = !pipe && n && iters > 1 && n <= copy_steps_max();
+    bool one = pipe || steps;          // all copies in one launch
     u64* bar = ctx->dev_tmp[dev] + 16;
     float ms = 0;
     double t0 = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        if (steps) HIPCK(hipMemsetAsync(bar, 0, 9 * 16 * sizeof(u64), s));   // global + 8 per-XCD counters
+        if (one) HIPCK(hipMemsetAsync(bar, 0, 9 * 16 * sizeof(u64), s));   // global + 8 per-XCD counters
         t0 = now_s();
         HIPCK(hipEventRecord(e0, s));
-        if (steps)
+        if (one && pipe)
+            HIPCK(launch_copy_pipe(dst, src, n, iters, bar, s, &grid));
+        else if (one)
             HIPCK(launch_copy_steps(dst, src, n, iters, bar, s, &grid));
         else
             for (int i = 0; i < iters && n; ++i) HIPCK(launch_copy(dst, src, n, s, &grid));
         HIPCK(hipEventRecord(e1, s));
         HIPCK(hipEventSynchronize(e1));
         HIPCK(hipEventElapsedTime(&ms, e0, e1));
-        if (!steps) break;
-        // k_copy_steps gave up on its grid barrier (bar[1], see the kernel):
+        if (!one) break;
+        // k_copy_steps / k_copy_pipe gave up on its grid barrier (bar[1]):
         // not every workgroup became resident — e.g. other ranks' persistent
         // transfer kernels hold CUs of this GPU.  Copy again, a launch per copy
         // (no residency needed); that is the call's result and its time.
@@ -1332,16 +1343,16 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
         HIPCK(hipStreamSynchronize(s));
         if (!stop) break;
         DBG("copy of %zu B: step barrier gave up, a launch per copy instead\n", n);
-        steps = false;
+        one = false;
     }
     t->wall_s = now_s() - t0;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     t->device_s = ms * 1e-3;
     t->bytes = (uint64_t)n * (uint64_t)iters;
-    t->launches = !n ? 0 : steps ? 1 : iters;
+    t->launches = !n ? 0 : one ? 1 : iters;
     t->nwg = grid;
-    t->protocol = steps ? kProtoCopySteps : kProtoCopy;
+    t->protocol = !one ? kProtoCopy : pipe ? kProtoCopyPipe : kProtoCopySteps;
     return MPX_OK;
 }
 

@@ -81,6 +81,36 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
         ctx.free(dst)
 
 
+@pytest.mark.parametrize("upl", [0, 1, 2, 8, 16])
+@pytest.mark.parametrize("iters", [1, 2, 3, 7])
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 4096 + 5, (1 << 20) + 3, (2 << 20) + 16, (4 << 20), (16 << 20) + 7])
+def test_copy_pipe_every_size_class(ctx, monkeypatch, n, iters, upl):
+    """k_copy_pipe (all copies in one launch; copy s+1's loads in flight
+    across copy s's grid barrier; a dedicated barrier wave), forced at every
+    size (MPX_COPY_PIPE_MAX) and units-per-lane choice (MPX_COPY_PIPE_UPL; 0 =
+    the default 4, widened until the grid stays resident): odd and even copy
+    counts (the loop is unrolled by two), a tail below 16 B with and without
+    a body, a grid of one: output against the oracle's pattern, nothing
+    written past the end."""
+    monkeypatch.setenv("MPX_COPY_PIPE_MAX", str(32 << 20))
+    if upl:
+        monkeypatch.setenv("MPX_COPY_PIPE_UPL", str(upl))
+    key = mpx.pattern_key(mpx.PATTERN_SEED, 2, 2, (n + upl) & 0xFFFF)
+    src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
+    try:
+        ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
+        ctx.fill(dst, n + 64, mpx.FILL_BYTE, 0xEE)
+        t = ctx.copy(0, dst, src, n, iters)
+        assert t.launches == 1 and mpx.PROTOCOLS.get(t.protocol) == ("copy_pipe" if iters > 1 else "copy"), \
+            t.protocol
+        assert ctx.checksum(dst, n) == O.pattern_checksum(n, mpx.FILL_SPLITMIX, key)
+        assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
+        assert t.bytes == n * iters
+    finally:
+        ctx.free(src)
+        ctx.free(dst)
+
+
 @pytest.mark.parametrize("n,grid", [(1, 1), (4096, 1), (16 << 10, 1), ((16 << 10) + 1, 2), (32 << 10, 4),
                                     (128 << 10, 16), ((128 << 10) + 16, 9), (512 << 10, 32), ((512 << 10) + 16, 33),
                                     (1 << 20, 64)])

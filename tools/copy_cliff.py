@@ -5,12 +5,15 @@
         under `rocprofv3 --kernel-trace --output-format csv -d <dir> -o cliff --`)
     python tools/copy_cliff.py summary <out.jsonl> <kernel_trace.csv>
 
-`run` measures every size with both forms of mpx_copy, in two states of the
+`run` measures every size with each form of mpx_copy, in two states of the
 process: "fresh", and "after_headline" (200 back-to-back 1 GiB copies, the
 headline's load, just before).  Per (state, size, form): one warm call, then
 5 calls of 10 copies, per-copy time from HIP events (best and median).  Forms:
   steps  : all copies in one k_copy_steps launch (MPX_COPY_STEPS_MAX raised)
   launch : one k_copy launch per copy (MPX_COPY_STEPS_MAX=0)
+  pipe*  : all copies in one k_copy_pipe launch (MPX_COPY_PIPE_MAX raised;
+           pipeN: N units per lane)
+(MPX_CLIFF_FORMS=steps,launch,pipe,... picks them; default steps,launch)
 and the in-kernel shader clock (tools/libclock_probe.so: delta s_memtime /
 delta s_memrealtime, MI355X_MICROARCH.md "DVFS give-back" item 6) before and
 after each state: one workgroup for 2 ms, and one per CU.
@@ -29,7 +32,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIZES = [512 << 10, 1 << 20, 2 << 20, 3 << 20, 4 << 20, 8 << 20, 16 << 20]
-FORMS = ("steps", "launch")
+# form -> environment of mpx_copy (read per call); MPX_CLIFF_FORMS=a,b,... selects
+FORMS = {
+    "steps": {"MPX_COPY_STEPS_MAX": str(16 << 20), "MPX_COPY_PIPE_MAX": "0"},
+    "launch": {"MPX_COPY_STEPS_MAX": "0", "MPX_COPY_PIPE_MAX": "0"},
+    "pipe": {"MPX_COPY_PIPE_MAX": str(16 << 20), "MPX_COPY_PIPE_UPL": ""},
+    "pipe2": {"MPX_COPY_PIPE_MAX": str(16 << 20), "MPX_COPY_PIPE_UPL": "2"},
+    "pipe8": {"MPX_COPY_PIPE_MAX": str(16 << 20), "MPX_COPY_PIPE_UPL": "8"},
+    "pipe16": {"MPX_COPY_PIPE_MAX": str(16 << 20), "MPX_COPY_PIPE_UPL": "16"},
+}
 CALLS, COPIES, WARM = 5, 10, 2
 EMPTY, EMPTY_COUNT = ((1, 64), (128, 256), (1024, 256), (4096, 256)), 20   # (grid, lanes) of empty launches
 G = 1 << 30
@@ -61,7 +72,7 @@ def run(out_path):
         c.fill(src, G, mpx.FILL_SPLITMIX, 11)
         for state in ("fresh", "after_headline"):
             if state == "after_headline":
-                os.environ["MPX_COPY_STEPS_MAX"] = "0"
+                os.environ.update(FORMS["launch"])
                 for _ in range(20):
                     c.copy(0, dst, src, G, 10)
                 schedule.append(dict(state=state, what="headline", dispatches=200))
@@ -70,8 +81,9 @@ def run(out_path):
                 probe.empty_kernels(0, grid, threads, EMPTY_COUNT)
             schedule.append(dict(state=state, what="empty"))
             for n in SIZES:
-                for form in FORMS:
-                    os.environ["MPX_COPY_STEPS_MAX"] = str(16 << 20) if form == "steps" else "0"
+                for form in os.environ.get("MPX_CLIFF_FORMS", "steps,launch").split(","):
+                    for k, v in FORMS[form].items():
+                        os.environ[k] = v
                     c.copy(0, dst, src, n, WARM)
                     per = []
                     for _ in range(CALLS):
@@ -110,13 +122,14 @@ def summary(lab_path, trace_path):
                                 kernel_us_median=round(statistics.median(dur), 3),
                                 gap_us_median=round(statistics.median(gap), 3)))
             continue
-        steps = item["path"] == "copy_steps"
+        steps = item["path"] in ("copy_steps", "copy_pipe")
         calls = []
         for copies in [WARM] + [COPIES] * CALLS:
             nd = 1 if steps else copies
             d = rows[k:k + nd]
             k += nd
-            assert all(("k_copy_steps" in r["Kernel_Name"]) == steps for r in d), (item, d[0]["Kernel_Name"])
+            assert all(("k_copy_steps" in r["Kernel_Name"] or "k_copy_pipe" in r["Kernel_Name"]) == steps
+                       for r in d), (item, d[0]["Kernel_Name"])
             s = [int(r["Start_Timestamp"]) for r in d]
             e = [int(r["End_Timestamp"]) for r in d]
             calls.append(dict(copies=copies, span_ns=e[-1] - s[0], kernel_ns=[b - a for a, b in zip(s, e)],
