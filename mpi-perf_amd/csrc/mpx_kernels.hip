@@ -1179,8 +1179,13 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     // resident grid: 5-wave workgroups, as many per CU as the VGPRs allow
     // (UPL 16: 208 VGPRs, one per CU; UPL 8: 112, three; UPL <= 4: six)
     auto cap_of = [](int u) -> size_t { return u >= 16 ? 256 : u >= 8 ? 512 : (size_t)kCopyPipeMaxGrid; };
-    int upl = 4;
-    if (const char* v = getenv("MPX_COPY_PIPE_UPL")) upl = atoi(v);   // A/B knob, read per call
+    // Units per lane: the grid barrier's cost grows with its arrivals (one
+    // per workgroup), so few wide workgroups win: 8 units up to 2 MiB, 16
+    // above (16-64 workgroups up to 4 MiB).  Per copy at 2 MiB: 64
+    // workgroups 2.11 us, 256 4.04, 512 7.8 (r03_copy_pipe_ab.jsonl).
+    int upl = n <= ((size_t)2 << 20) ? 8 : 16;
+    if (const char* v = getenv("MPX_COPY_PIPE_UPL"))   // A/B knob, read per call
+        if (*v) upl = atoi(v);
     upl = upl <= 1 ? 1 : upl <= 2 ? 2 : upl <= 4 ? 4 : upl <= 8 ? 8 : 16;
     size_t grid = (n16 + lanes * upl - 1) / (lanes * upl);
     while (grid > cap_of(upl) && upl < 16) {

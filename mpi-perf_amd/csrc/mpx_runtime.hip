@@ -298,11 +298,16 @@ size_t copy_steps_max() {
     return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyStepsDefaultMax;
 }
 
-// Largest copy whose iterations run in one k_copy_pipe launch
-// (MPX_COPY_PIPE_MAX bytes, read per call; 0 = never)
+// Copies of (kCopyPipeDefaultMin, kCopyPipeDefaultMax] bytes run all their
+// iterations in one k_copy_pipe launch (MPX_COPY_PIPE_MIN / MPX_COPY_PIPE_MAX
+// override, read per call; MAX = 0: never).
+size_t copy_pipe_min() {
+    const char* v = getenv("MPX_COPY_PIPE_MIN");
+    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyPipeDefaultMin;
+}
 size_t copy_pipe_max() {
     const char* v = getenv("MPX_COPY_PIPE_MAX");
-    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)0;
+    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyPipeDefaultMax;
 }
 
 // the receives the reference's non-blocking loop completes (Waitall) for
@@ -1312,9 +1317,11 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     HIPCK(hipEventCreate(&e0));
     HIPCK(hipEventCreate(&e1));
     int grid = 0;
-    // copies of <= copy_steps_max() bytes run all iterations in one launch
-    // (k_copy_steps: dispatch-bound sizes); larger ones one k_copy launch each
-    const bool pipe = n && iters > 1 && n <= copy_pipe_max();
+    // All iterations in one launch where a launch per copy is dispatch-bound:
+    // k_copy_pipe above 512 KiB to 8 MiB, k_copy_steps up to 512 KiB (and up
+    // to copy_steps_max() where the pipe is off); one k_copy launch per copy
+    // above (profiles/r03_copy_pipe_ab.jsonl)
+    const bool pipe = n && iters > 1 && n > copy_pipe_min() && n <= copy_pipe_max();
     bool steps = !pipe && n && iters > 1 && n <= copy_steps_max();
     bool one = pipe || steps;          // all copies in one launch
     u64* bar = ctx->dev_tmp[dev] + 16;

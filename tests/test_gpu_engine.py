@@ -57,6 +57,7 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
     workgroup on one XCD) at 1 MiB + 3:
     output against the oracle's pattern, nothing written past the end."""
     monkeypatch.setenv("MPX_COPY_STEPS_MAX", str(16 << 20))
+    monkeypatch.setenv("MPX_COPY_PIPE_MAX", "0")
     key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
     try:
@@ -93,6 +94,7 @@ def test_copy_pipe_every_size_class(ctx, monkeypatch, n, iters, upl):
     a body, a grid of one: output against the oracle's pattern, nothing
     written past the end."""
     monkeypatch.setenv("MPX_COPY_PIPE_MAX", str(32 << 20))
+    monkeypatch.setenv("MPX_COPY_PIPE_MIN", "0")
     if upl:
         monkeypatch.setenv("MPX_COPY_PIPE_UPL", str(upl))
     key = mpx.pattern_key(mpx.PATTERN_SEED, 2, 2, (n + upl) & 0xFFFF)
@@ -114,11 +116,13 @@ def test_copy_pipe_every_size_class(ctx, monkeypatch, n, iters, upl):
 @pytest.mark.parametrize("n,grid", [(1, 1), (4096, 1), (16 << 10, 1), ((16 << 10) + 1, 2), (32 << 10, 4),
                                     (128 << 10, 16), ((128 << 10) + 16, 9), (512 << 10, 32), ((512 << 10) + 16, 33),
                                     (1 << 20, 64)])
-def test_copy_steps_grid_rule(ctx, n, grid):
-    """The one-launch copy's default shape (mpx_kernels.hip launch_copy_steps):
-    one 1024-lane workgroup up to 16 KiB; 512-lane workgroups on one XCD to
+def test_copy_steps_grid_rule(ctx, monkeypatch, n, grid):
+    """The k_copy_steps shape (mpx_kernels.hip launch_copy_steps): one
+    1024-lane workgroup up to 16 KiB; 512-lane workgroups on one XCD to
     128 KiB, 1024-lane ones on one XCD to 512 KiB; up to 64 1024-lane
-    workgroups over every XCD to 1 MiB.  timing.nwg = working workgroups."""
+    workgroups over every XCD to 1 MiB (above 512 KiB only with the pipe off,
+    as here).  timing.nwg = working workgroups."""
+    monkeypatch.setenv("MPX_COPY_PIPE_MAX", "0")
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n)
     try:
         ctx.fill(src, n, mpx.FILL_BYTE, 0x5C)
@@ -128,6 +132,32 @@ def test_copy_steps_grid_rule(ctx, n, grid):
     finally:
         ctx.free(src)
         ctx.free(dst)
+
+
+@pytest.mark.parametrize("n,grid", [((512 << 10) + 16, 17), (1 << 20, 32), (2 << 20, 64), ((2 << 20) + 16, 33),
+                                    (3 << 20, 48), (4 << 20, 64), (8 << 20, 128)])
+def test_copy_pipe_grid_rule(ctx, n, grid):
+    """The default one-launch form above 512 KiB to 8 MiB (k_copy_pipe):
+    320-lane workgroups (four copy waves + the barrier wave), 8 units per
+    lane up to 2 MiB and 16 above, so 16-64 workgroups arrive at the grid
+    barrier up to 4 MiB.  timing.nwg = workgroups."""
+    src, dst = ctx.alloc(0, n), ctx.alloc(0, n)
+    try:
+        ctx.fill(src, n, mpx.FILL_BYTE, 0x5D)
+        t = ctx.copy(0, dst, src, n, 3)
+        assert (mpx.PROTOCOLS[t.protocol], t.nwg, t.launches) == ("copy_pipe", grid, 1)
+        assert ctx.checksum(dst, n) == ctx.checksum(src, n)
+    finally:
+        ctx.free(src)
+        ctx.free(dst)
+
+
+def copy_path(n: int, iters: int) -> str:
+    """mpx_copy's default form: one launch for all copies (k_copy_steps up to
+    512 KiB, k_copy_pipe to 8 MiB), a k_copy launch per copy above"""
+    if not n or iters < 2 or n > (8 << 20):
+        return "copy"
+    return "copy_steps" if n <= (512 << 10) else "copy_pipe"
 
 
 @pytest.mark.parametrize("n", SIZES)
@@ -142,11 +172,11 @@ def test_copy_kernel_matches_oracle(ctx, n):
         # nothing written past the end
         assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
         assert t.bytes == 2 * n
-        # both copies in one k_copy_steps launch up to 1 MiB, a launch each above
-        steps = 0 < n <= (1 << 20)
-        assert t.launches == (1 if steps else 2 if n else 0)
+        # both copies in one launch up to 8 MiB, a launch each above
+        one = copy_path(n, 2) != "copy"
+        assert t.launches == (1 if one else 2 if n else 0)
         if n:
-            assert mpx.PROTOCOLS[t.protocol] == ("copy_steps" if steps else "copy")
+            assert mpx.PROTOCOLS[t.protocol] == copy_path(n, 2)
     finally:
         ctx.free(src)
         ctx.free(dst)
