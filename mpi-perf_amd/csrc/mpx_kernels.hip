@@ -139,9 +139,12 @@ constexpr int kCopyStepsBatch = 8;
 template <int T, bool XCD>
 __global__ __launch_bounds__(T) void k_copy_steps(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n16,
                                                  unsigned tail, int iters, u64* bar, int drain, int one_xcd) {
-    // one_xcd (A/B): the grid is 8x the working workgroups and only those
-    // dispatched to XCD 0 (blockIdx % 8 == 0, round-robin dispatch) work, so
-    // every barrier arrival comes from one XCD; the rest exit at once
+    // one_xcd: the grid is 8x the working workgroups and only those with
+    // blockIdx % 8 == 0 work (the rest exit at once), so that with the
+    // round-robin dispatch seen on gfx950 every barrier arrival comes from
+    // XCD 0.  A placement heuristic, speed only: dispatch -> XCD placement is
+    // undefined (MI355X_MICROARCH.md), and the working set is correct
+    // wherever it lands (sized to stay resident; the barrier is bounded)
     if (one_xcd && (blockIdx.x & 7)) return;
     const unsigned wg = one_xcd ? blockIdx.x >> 3 : blockIdx.x;
     const u64 g = one_xcd ? gridDim.x >> 3 : gridDim.x;
