@@ -1198,6 +1198,8 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     if (grid > cap_of(upl) || n >= ((size_t)1 << 32)) return hipErrorInvalidValue;
     if (grid < 1) grid = 1;
     if (grid_out) *grid_out = (int)grid;
+    // (nontemporal loads: default-policy ones read the same, fresh or after
+    // 1 GiB copies, 2-8 MiB within 0.03 us: profiles/r03_copy_pipe_state.jsonl)
     void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*) =
         upl <= 1 ? k_copy_pipe<1> : upl <= 2 ? k_copy_pipe<2> : upl <= 4 ? k_copy_pipe<4>
         : upl <= 8 ? k_copy_pipe<8> : k_copy_pipe<16>;
