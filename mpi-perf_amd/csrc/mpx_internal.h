@@ -172,17 +172,17 @@ constexpr int kCopyStepsMaxGrid = 1024;   // 4 workgroups per CU: always co-resi
 // the switch stays at 1 MiB; above it a launch per copy is as fast or faster
 // (16 MiB 4.22 vs 5.15-5.95; r02_copy_steps_upl.jsonl, r02_copy_steps_mid.jsonl)
 constexpr size_t kCopyStepsDefaultMax = (size_t)1 << 20;
-// k_copy_pipe's range: (512 KiB, 4 MiB].  Per copy (HIP events, best of 5
-// calls of 10): 1 MiB 1.69-1.72 us (k_copy_steps 2.0, a launch per copy
-// 2.3-2.9), 2 MiB 2.10-2.16 (2.4 / 2.4-3.1), 3 MiB 2.36-2.49 (2.8 / 2.9-3.1),
-// 4 MiB 2.54-2.60 (3.0 / 2.9-5.8) on three boxes, fresh and after 1 GiB
-// copies; on one box 4 MiB read 3.1-4.3 right after 1 GiB copies, where
-// steps read 3.0 and a launch per copy 4.2.  512 KiB: 1.56 vs the one-XCD
-// steps form's 1.64 (kept).  From 6 MiB a launch per copy wins (6 MiB 2.93
-// vs 3.07-3.11, 8 MiB 3.1-3.9 vs 3.5-6.5: the 96-128-workgroup barrier)
-// (profiles/r03_copy_pipe_ab.jsonl, r03_copy_pipe_state.jsonl)
+// k_copy_pipe's range: (512 KiB, 2 MiB].  Per copy (HIP events, best of 5
+// calls of 10) on four boxes, fresh and right after 1 GiB copies: 1 MiB
+// 1.67-1.74 us (k_copy_steps 2.0, a launch per copy 2.3-2.9), 2 MiB
+// 2.10-2.18 (2.4 / 2.4-3.1) — but 3.14 inside one box's bench.py sweep.
+// At 4 MiB it is 2.54-2.60 fresh and 4.3-4.7 right after 1 GiB copies on
+// two of four boxes, where a launch per copy stays at 2.8-3.0: above 2 MiB
+// the launch per copy is the robust choice.  512 KiB: 1.56 vs the one-XCD
+// steps form's 1.64 (kept).  The barrier words in fine-grained or uncached
+// memory do not remove the state effect (r03_copy_pipe_state.jsonl).
 constexpr size_t kCopyPipeDefaultMin = (size_t)512 << 10;
-constexpr size_t kCopyPipeDefaultMax = (size_t)4 << 20;
+constexpr size_t kCopyPipeDefaultMax = (size_t)2 << 20;
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
                              int* grid_out);
 // all `iters` copies in one k_copy_pipe launch (copy s+1's loads in flight

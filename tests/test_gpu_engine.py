@@ -134,13 +134,14 @@ def test_copy_steps_grid_rule(ctx, monkeypatch, n, grid):
         ctx.free(dst)
 
 
-@pytest.mark.parametrize("n,grid", [((512 << 10) + 16, 17), (1 << 20, 32), (2 << 20, 64), ((2 << 20) + 16, 33),
-                                    (3 << 20, 48), (4 << 20, 64)])
-def test_copy_pipe_grid_rule(ctx, n, grid):
-    """The default one-launch form above 512 KiB to 4 MiB (k_copy_pipe):
+@pytest.mark.parametrize("n,grid", [((512 << 10) + 16, 17), (1 << 20, 32), ((1 << 20) + 16, 33), (2 << 20, 64),
+                                    ((2 << 20) + 16, 33), (3 << 20, 48), (4 << 20, 64)])
+def test_copy_pipe_grid_rule(ctx, monkeypatch, n, grid):
+    """The one-launch form of 512 KiB - 2 MiB (k_copy_pipe; to 4 MiB here):
     320-lane workgroups (four copy waves + the barrier wave), 8 units per
     lane up to 2 MiB and 16 above, so 16-64 workgroups arrive at the grid
     barrier up to 4 MiB.  timing.nwg = workgroups."""
+    monkeypatch.setenv("MPX_COPY_PIPE_MAX", str(4 << 20))
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n)
     try:
         ctx.fill(src, n, mpx.FILL_BYTE, 0x5D)
@@ -154,8 +155,8 @@ def test_copy_pipe_grid_rule(ctx, n, grid):
 
 def copy_path(n: int, iters: int) -> str:
     """mpx_copy's default form: one launch for all copies (k_copy_steps up to
-    512 KiB, k_copy_pipe to 4 MiB), a k_copy launch per copy above"""
-    if not n or iters < 2 or n > (4 << 20):
+    512 KiB, k_copy_pipe to 2 MiB), a k_copy launch per copy above"""
+    if not n or iters < 2 or n > (2 << 20):
         return "copy"
     return "copy_steps" if n <= (512 << 10) else "copy_pipe"
 
@@ -172,7 +173,7 @@ def test_copy_kernel_matches_oracle(ctx, n):
         # nothing written past the end
         assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
         assert t.bytes == 2 * n
-        # both copies in one launch up to 4 MiB, a launch each above
+        # both copies in one launch up to 2 MiB, a launch each above
         one = copy_path(n, 2) != "copy"
         assert t.launches == (1 if one else 2 if n else 0)
         if n:
