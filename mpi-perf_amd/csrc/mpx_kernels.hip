@@ -252,19 +252,47 @@ template <int UPL>
 // (no __restrict__ on src: with it the optimiser may assume src's bytes never
 // change during the kernel and keep the first copy's values for every copy)
 __global__ __launch_bounds__(kPipeThreads) void k_copy_pipe(const v4u* src, v4u* dst,
-                                                          size_t n16, unsigned tail, int iters, u64* bar) {
+                                                          size_t n16, unsigned tail, int iters, u64* bar,
+                                                          int hier) {
     __shared__ int s_stop;
     if (threadIdx.x >= kPipeCopyWaves * 64) {
-        // the barrier wave: one grid barrier per copy boundary
+        // the barrier wave: one grid barrier per copy boundary.  hier = 0:
+        // one counter (bar[0]) that every workgroup counts in on and polls.
+        // hier = 1 (A/B): workgroup b counts in on its group's counter
+        // bar[16 (1 + b % 8)]; the last of a group counts the group in on
+        // bar[0]; the last group writes every group's release word
+        // bar[16 (9 + g)], which that group's workgroups poll — 8 same-address
+        // queues in parallel instead of one.
+        const unsigned grid = gridDim.x;
+        const unsigned g = blockIdx.x & 7;
+        const u64 ng = (grid - g + 7) / 8;                   // workgroups in group g
+        const u64 groups = grid < 8 ? grid : 8;
         for (int s = 0; s + 1 < iters; ++s) {
             wg_barrier_nofence();                      // every copy wave issued copy s's stores
             if (threadIdx.x == kPipeCopyWaves * 64) {
                 s_stop = 0;
-                __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const u64 want = (u64)gridDim.x * (u64)(s + 1);
+                u64 want;
+                const u64* poll;
+                if (hier) {
+                    const u64 old = __hip_atomic_fetch_add(bar + 16 * (1 + g), 1ull, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                    if (old + 1 == ng * (u64)(s + 1)) {
+                        const u64 t = __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (t + 1 == groups * (u64)(s + 1))
+                            for (u64 k = 0; k < groups; ++k)
+                                __hip_atomic_store(bar + 16 * (9 + k), (u64)(s + 1), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    want = (u64)(s + 1);
+                    poll = bar + 16 * (9 + g);
+                } else {
+                    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    want = (u64)grid * (u64)(s + 1);
+                    poll = bar;
+                }
                 const u64 t0 = now_ticks();
                 u64 spins = 0;
-                while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                while (__hip_atomic_load(poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
                     if ((++spins & 255) == 0 && now_ticks() - t0 > 100000000ull) {
                         // 1 s: a workgroup never arrived (bar[1] -> mpx_copy's fallback)
                         __hip_atomic_store(&bar[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1200,12 +1228,15 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     if (grid_out) *grid_out = (int)grid;
     // (nontemporal loads: default-policy ones read the same, fresh or after
     // 1 GiB copies, 2-8 MiB within 0.03 us: profiles/r03_copy_pipe_state.jsonl)
-    void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*) =
+    void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*, int) =
         upl <= 1 ? k_copy_pipe<1> : upl <= 2 ? k_copy_pipe<2> : upl <= 4 ? k_copy_pipe<4>
         : upl <= 8 ? k_copy_pipe<8> : k_copy_pipe<16>;
+    int hier = 0;   // MPX_COPY_PIPE_HIER=1: two-level barrier (A/B knob, read per call)
+    if (const char* v = getenv("MPX_COPY_PIPE_HIER"))
+        if (*v) hier = atoi(v) != 0;
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kPipeThreads), 0, s, reinterpret_cast<const v4u*>(src),
-                       reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters, bar);
+                       reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters, bar, hier);
     return hipGetLastError();
 }
 

@@ -176,8 +176,9 @@ int util_stream(mpx_ctx* ctx, int dev, hipStream_t* s) {
     hipStream_t st;
     HIPCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     u64* tmp;
-    // [0] checksum sum; [16 ..) k_copy_steps' barrier: 9 counters 128 B apart
-    HIPCK(hipMalloc(&tmp, 16 * 10 * sizeof(u64)));
+    // [0] checksum sum; [16 ..) the one-launch copies' barrier: 17 words
+    // 128 B apart (top counter, 8 group counters, 8 release words)
+    HIPCK(hipMalloc(&tmp, 16 * 19 * sizeof(u64)));
     ctx->dev_stream[dev] = st;
     ctx->dev_tmp[dev] = tmp;
     *s = st;
@@ -1328,7 +1329,7 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     float ms = 0;
     double t0 = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        if (one) HIPCK(hipMemsetAsync(bar, 0, 9 * 16 * sizeof(u64), s));   // global + 8 per-XCD counters
+        if (one) HIPCK(hipMemsetAsync(bar, 0, 17 * 16 * sizeof(u64), s));   // top + 8 group counters + 8 release words
         t0 = now_s();
         HIPCK(hipEventRecord(e0, s));
         if (one && pipe)

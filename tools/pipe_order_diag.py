@@ -11,11 +11,13 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 import mpx  # noqa: E402
 
 G = 1 << 30
-ARMS = {"pipe": {}, "pipe_barfine": {"MPX_COPY_BAR": "fine"}, "pipe_barunc": {"MPX_COPY_BAR": "uncached"},
-        "steps_barunc": {"MPX_COPY_PIPE_MAX": "0", "MPX_COPY_STEPS_MAX": str(16 << 20), "MPX_COPY_BAR": "uncached"},
-        "steps": {"MPX_COPY_PIPE_MAX": "0", "MPX_COPY_STEPS_MAX": str(16 << 20)},
+BIG = {"MPX_COPY_PIPE_MAX": str(32 << 20)}
+ARMS = {"pipe": BIG, "hier_u2": dict(BIG, MPX_COPY_PIPE_HIER="1", MPX_COPY_PIPE_UPL="2"),
+        "hier_u4": dict(BIG, MPX_COPY_PIPE_HIER="1", MPX_COPY_PIPE_UPL="4"),
+        "hier_u8": dict(BIG, MPX_COPY_PIPE_HIER="1", MPX_COPY_PIPE_UPL="8"),
+        "hier_u16": dict(BIG, MPX_COPY_PIPE_HIER="1", MPX_COPY_PIPE_UPL="16"),
         "launch": {"MPX_COPY_PIPE_MAX": "0", "MPX_COPY_STEPS_MAX": "0"}}
-KEYS = ("MPX_COPY_PIPE_UPL", "MPX_COPY_BAR", "MPX_COPY_PIPE_MAX", "MPX_COPY_STEPS_MAX")
+KEYS = ("MPX_COPY_PIPE_UPL", "MPX_COPY_PIPE_HIER", "MPX_COPY_PIPE_MAX", "MPX_COPY_STEPS_MAX")
 
 
 def best(c, src, dst, n, copies=10):
@@ -30,13 +32,13 @@ def best(c, src, dst, n, copies=10):
 with mpx.Context(1) as c:
     src, dst = c.alloc(0, G), c.alloc(0, G)
     c.fill(src, G, mpx.FILL_SPLITMIX, 3)
-    for state in ("fresh", "after 30 x 1 GiB", "after 30 x 1 GiB (again)", "after 30 x 1 GiB (third)"):
+    for state in ("fresh", "after 30 x 1 GiB"):
         if state != "fresh":
             for k in KEYS:
                 os.environ.pop(k, None)
             for _ in range(3):
                 c.copy(0, dst, src, G, 10)
-        for n in (1 << 20, 2 << 20, 4 << 20):
+        for n in (1 << 20, 2 << 20, 4 << 20, 8 << 20, 16 << 20):
             for arm, env in ARMS.items():
                 for k in KEYS:
                     os.environ.pop(k, None)
