@@ -128,7 +128,7 @@ def copy_sweep(mpx, c, src, dst, nbytes: int) -> dict:
     """BASELINE config 2's sweep beside the headline: B = 2^k for 1 B ..
     nbytes.  Each size: one mpx_copy call of 10 copies (3 at >= 256 MiB)
     timed with HIP events on the copy's stream, best of 5 such calls; per
-    copy = call time / copies.  Up to 2 MiB the call is ONE launch (all
+    copy = call time / copies.  Up to 16 MiB the call is ONE launch (all
     copies, a grid barrier between them: k_copy_steps to 512 KiB, k_copy_pipe
     above), above it one k_copy launch per copy ("path").  `hbm_GBps` counts 2B per copy; `frac` is that
     over the 8 TB/s HBM peak — below ~256 MiB a repeated copy of the same

@@ -172,17 +172,19 @@ constexpr int kCopyStepsMaxGrid = 1024;   // 4 workgroups per CU: always co-resi
 // the switch stays at 1 MiB; above it a launch per copy is as fast or faster
 // (16 MiB 4.22 vs 5.15-5.95; r02_copy_steps_upl.jsonl, r02_copy_steps_mid.jsonl)
 constexpr size_t kCopyStepsDefaultMax = (size_t)1 << 20;
-// k_copy_pipe's range: (512 KiB, 2 MiB].  Per copy (HIP events, best of 5
-// calls of 10) on four boxes, fresh and right after 1 GiB copies: 1 MiB
-// 1.67-1.74 us (k_copy_steps 2.0, a launch per copy 2.3-2.9), 2 MiB
-// 2.10-2.18 (2.4 / 2.4-3.1) — but 3.14 inside one box's bench.py sweep.
-// At 4 MiB it is 2.54-2.60 fresh and 4.3-4.7 right after 1 GiB copies on
-// two of four boxes, where a launch per copy stays at 2.8-3.0: above 2 MiB
-// the launch per copy is the robust choice.  512 KiB: 1.56 vs the one-XCD
-// steps form's 1.64 (kept).  The barrier words in fine-grained or uncached
-// memory do not remove the state effect (r03_copy_pipe_state.jsonl).
+// k_copy_pipe's range: (512 KiB, 16 MiB].  Per copy (HIP events, best of 5
+// calls of 10), fresh and right after 1 GiB copies, on four boxes: 1 MiB
+// 1.67-2.11 us (k_copy_steps 2.0, a launch per copy 2.3-3.0), 2 MiB 2.08-2.18
+// (2.4 / 2.4-3.1; one box's bench sweep read 3.14); above 2 MiB with the
+// two-level barrier and ~256 workgroups: 4 MiB 2.56-2.60 (launch 2.9-3.0),
+// 8 MiB 3.2-3.4 (3.2-3.7), 16 MiB 4.3-4.9 (5.0-5.2).  The one-counter form
+// with few wide workgroups was state-sensitive above 2 MiB (4 MiB 4.3-4.7
+// after 1 GiB copies on two boxes, 8 MiB 6.2).  512 KiB: 1.56 vs the
+// one-XCD steps form's 1.64 (kept).  A grid of 16 MiB / 256 workgroups is
+// the resident limit of 16 units per lane (r03_copy_pipe_ab.jsonl,
+// r03_copy_pipe_state.jsonl, r03_copy_pipe_hier.jsonl).
 constexpr size_t kCopyPipeDefaultMin = (size_t)512 << 10;
-constexpr size_t kCopyPipeDefaultMax = (size_t)2 << 20;
+constexpr size_t kCopyPipeDefaultMax = (size_t)16 << 20;
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
                              int* grid_out);
 // all `iters` copies in one k_copy_pipe launch (copy s+1's loads in flight

@@ -1210,11 +1210,17 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     // resident grid: 5-wave workgroups, as many per CU as the VGPRs allow
     // (UPL 16: 208 VGPRs, one per CU; UPL 8: 112, three; UPL <= 4: six)
     auto cap_of = [](int u) -> size_t { return u >= 16 ? 256 : u >= 8 ? 512 : (size_t)kCopyPipeMaxGrid; };
-    // Units per lane: the grid barrier's cost grows with its arrivals (one
-    // per workgroup), so few wide workgroups win: 8 units up to 2 MiB, 16
-    // above (16-64 workgroups up to 4 MiB).  Per copy at 2 MiB: 64
-    // workgroups 2.11 us, 256 4.04, 512 7.8 (r03_copy_pipe_ab.jsonl).
-    int upl = n <= ((size_t)2 << 20) ? 8 : 16;
+    // Shape.  Up to 2 MiB: 8 units per lane and one barrier counter — few
+    // wide workgroups (16-64), because one counter's cost grows with its
+    // arrivals (at 2 MiB: 64 workgroups 2.11 us per copy, 256 4.04, 512 7.8;
+    // r03_copy_pipe_ab.jsonl).  Above: the two-level barrier (8 group
+    // counters in parallel, per-group release words) with about 256
+    // workgroups, 4-16 units per lane: 8 MiB 3.2-3.4 us and 16 MiB 4.3-4.9
+    // against 3.2-3.7 / 5.0-5.2 for a launch per copy, where the one-counter
+    // pipe read 3.6-6.2 / 12-13 (r03_copy_pipe_hier.jsonl).
+    const bool big = n > ((size_t)2 << 20);
+    int upl = big ? 4 : 8;
+    while (big && upl < 16 && (n16 + lanes * upl - 1) / (lanes * upl) > 256) upl *= 2;
     if (const char* v = getenv("MPX_COPY_PIPE_UPL"))   // A/B knob, read per call
         if (*v) upl = atoi(v);
     upl = upl <= 1 ? 1 : upl <= 2 ? 2 : upl <= 4 ? 4 : upl <= 8 ? 8 : 16;
@@ -1231,7 +1237,7 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*, int) =
         upl <= 1 ? k_copy_pipe<1> : upl <= 2 ? k_copy_pipe<2> : upl <= 4 ? k_copy_pipe<4>
         : upl <= 8 ? k_copy_pipe<8> : k_copy_pipe<16>;
-    int hier = 0;   // MPX_COPY_PIPE_HIER=1: two-level barrier (A/B knob, read per call)
+    int hier = big ? 1 : 0;   // MPX_COPY_PIPE_HIER=0|1 forces the barrier form (A/B knob, read per call)
     if (const char* v = getenv("MPX_COPY_PIPE_HIER"))
         if (*v) hier = atoi(v) != 0;
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call

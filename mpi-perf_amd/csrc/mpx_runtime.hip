@@ -1319,7 +1319,7 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     HIPCK(hipEventCreate(&e1));
     int grid = 0;
     // All iterations in one launch where a launch per copy is dispatch-bound:
-    // k_copy_pipe above 512 KiB to 2 MiB, k_copy_steps up to 512 KiB (and up
+    // k_copy_pipe above 512 KiB to 16 MiB, k_copy_steps up to 512 KiB (and up
     // to copy_steps_max() where the pipe is off); one k_copy launch per copy
     // above (profiles/r03_copy_pipe_ab.jsonl)
     const bool pipe = n && iters > 1 && n > copy_pipe_min() && n <= copy_pipe_max();

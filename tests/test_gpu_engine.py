@@ -135,13 +135,14 @@ def test_copy_steps_grid_rule(ctx, monkeypatch, n, grid):
 
 
 @pytest.mark.parametrize("n,grid", [((512 << 10) + 16, 17), (1 << 20, 32), ((1 << 20) + 16, 33), (2 << 20, 64),
-                                    ((2 << 20) + 16, 33), (3 << 20, 48), (4 << 20, 64)])
-def test_copy_pipe_grid_rule(ctx, monkeypatch, n, grid):
-    """The one-launch form of 512 KiB - 2 MiB (k_copy_pipe; to 4 MiB here):
-    320-lane workgroups (four copy waves + the barrier wave), 8 units per
-    lane up to 2 MiB and 16 above, so 16-64 workgroups arrive at the grid
-    barrier up to 4 MiB.  timing.nwg = workgroups."""
-    monkeypatch.setenv("MPX_COPY_PIPE_MAX", str(4 << 20))
+                                    ((2 << 20) + 16, 129), (3 << 20, 192), (4 << 20, 256), (8 << 20, 256),
+                                    ((8 << 20) + 16, 129), (16 << 20, 256)])
+def test_copy_pipe_grid_rule(ctx, n, grid):
+    """The one-launch form of 512 KiB - 16 MiB (k_copy_pipe): 320-lane
+    workgroups (four copy waves + the barrier wave); up to 2 MiB 8 units per
+    lane and one barrier counter (16-64 workgroups), above it the two-level
+    barrier with up to 256 workgroups of 4-16 units per lane.
+    timing.nwg = workgroups."""
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n)
     try:
         ctx.fill(src, n, mpx.FILL_BYTE, 0x5D)
@@ -153,10 +154,37 @@ def test_copy_pipe_grid_rule(ctx, monkeypatch, n, grid):
         ctx.free(dst)
 
 
+@pytest.mark.parametrize("hier", ["0", "1"])
+@pytest.mark.parametrize("iters", [2, 5])
+@pytest.mark.parametrize("n,upl", [(16, 1), (4096 * 5 + 3, 1), (256 << 10, 16), ((256 << 10) + 16, 1),
+                                   ((1 << 20) + 7, 2), (9 << 20, 16), ((2 << 20) + 48, 4)])
+def test_copy_pipe_barrier_forms(ctx, monkeypatch, n, upl, iters, hier):
+    """Both grid-barrier forms of k_copy_pipe (one counter; 8 group counters
+    + release words) at grids of 1, 5, 4 (fewer workgroups than groups), 65,
+    129 (groups of unequal size), 128 and 144 workgroups, odd and even copy
+    counts: output against the oracle, nothing written past the end."""
+    monkeypatch.setenv("MPX_COPY_PIPE_MAX", str(32 << 20))
+    monkeypatch.setenv("MPX_COPY_PIPE_MIN", "0")
+    monkeypatch.setenv("MPX_COPY_PIPE_UPL", str(upl))
+    monkeypatch.setenv("MPX_COPY_PIPE_HIER", hier)
+    key = mpx.pattern_key(mpx.PATTERN_SEED, 3, 3, (n + iters) & 0xFFFF)
+    src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
+    try:
+        ctx.fill(src, n, mpx.FILL_SPLITMIX, key)
+        ctx.fill(dst, n + 64, mpx.FILL_BYTE, 0xEE)
+        t = ctx.copy(0, dst, src, n, iters)
+        assert mpx.PROTOCOLS[t.protocol] == "copy_pipe" and t.launches == 1
+        assert ctx.checksum(dst, n) == O.pattern_checksum(n, mpx.FILL_SPLITMIX, key)
+        assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
+    finally:
+        ctx.free(src)
+        ctx.free(dst)
+
+
 def copy_path(n: int, iters: int) -> str:
     """mpx_copy's default form: one launch for all copies (k_copy_steps up to
-    512 KiB, k_copy_pipe to 2 MiB), a k_copy launch per copy above"""
-    if not n or iters < 2 or n > (2 << 20):
+    512 KiB, k_copy_pipe to 16 MiB), a k_copy launch per copy above"""
+    if not n or iters < 2 or n > (16 << 20):
         return "copy"
     return "copy_steps" if n <= (512 << 10) else "copy_pipe"
 
@@ -173,7 +201,7 @@ def test_copy_kernel_matches_oracle(ctx, n):
         # nothing written past the end
         assert ctx.read(dst, 64, offset=n) == b"\xee" * 64
         assert t.bytes == 2 * n
-        # both copies in one launch up to 2 MiB, a launch each above
+        # both copies in one launch up to 16 MiB, a launch each above
         one = copy_path(n, 2) != "copy"
         assert t.launches == (1 if one else 2 if n else 0)
         if n:

@@ -1,7 +1,7 @@
-"""Diagnostic: k_copy_pipe per-copy time at 1-8 MiB in a fresh process and
+"""Diagnostic: k_copy_pipe per-copy time at 1-16 MiB in a fresh process and
 right after 1 GiB copies (the state bench.py's sweep runs in), per units
-per lane and load policy (MPX_COPY_PIPE_UPL, MPX_COPY_PIPE_LDNT), against
-k_copy_steps and a launch per copy.  JSON lines."""
+per lane and barrier form (MPX_COPY_PIPE_UPL, MPX_COPY_PIPE_HIER), against a
+launch per copy.  JSON lines."""
 import json
 import os
 import sys
