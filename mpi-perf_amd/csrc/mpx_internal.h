@@ -172,16 +172,13 @@ constexpr int kCopyStepsMaxGrid = 1024;   // 4 workgroups per CU: always co-resi
 // the switch stays at 1 MiB; above it a launch per copy is as fast or faster
 // (16 MiB 4.22 vs 5.15-5.95; r02_copy_steps_upl.jsonl, r02_copy_steps_mid.jsonl)
 constexpr size_t kCopyStepsDefaultMax = (size_t)1 << 20;
-// k_copy_pipe's range: (512 KiB, 16 MiB].  Per copy (HIP events, best of 5
-// calls of 10), fresh and right after 1 GiB copies, on four boxes: 1 MiB
-// 1.67-2.11 us (k_copy_steps 2.0, a launch per copy 2.3-3.0), 2 MiB 2.08-2.18
-// (2.4 / 2.4-3.1; one box's bench sweep read 3.14); above 2 MiB with the
-// two-level barrier and ~256 workgroups: 4 MiB 2.56-2.60 (launch 2.9-3.0),
-// 8 MiB 3.2-3.4 (3.2-3.7), 16 MiB 4.3-4.9 (5.0-5.2).  The one-counter form
-// with few wide workgroups was state-sensitive above 2 MiB (4 MiB 4.3-4.7
-// after 1 GiB copies on two boxes, 8 MiB 6.2).  512 KiB: 1.56 vs the
-// one-XCD steps form's 1.64 (kept).  A grid of 16 MiB / 256 workgroups is
-// the resident limit of 16 units per lane (r03_copy_pipe_ab.jsonl,
+// k_copy_pipe's range: (512 KiB, 16 MiB] (shape rule and numbers at
+// launch_copy_pipe).  Per copy, in bench.py's sweep (right after the 1 GiB
+// headline) and in fresh processes, against k_copy_steps / a launch per
+// copy: 1 MiB 1.67-2.1 us (2.0 / 2.3-3.0), 4 MiB 2.56-2.59 (3.0 / 2.9-3.0),
+// 8 MiB 3.2-3.9 (4.2 / 3.2-4.2), 16 MiB 4.3-6.0 (- / 5.0-6.8).  512 KiB:
+// 1.56 vs the one-XCD steps form's 1.64 (kept).  16 MiB is the resident
+// limit of 256 workgroups x 16 units per lane (r03_copy_pipe_ab.jsonl,
 // r03_copy_pipe_state.jsonl, r03_copy_pipe_hier.jsonl).
 constexpr size_t kCopyPipeDefaultMin = (size_t)512 << 10;
 constexpr size_t kCopyPipeDefaultMax = (size_t)16 << 20;

@@ -1210,15 +1210,18 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     // resident grid: 5-wave workgroups, as many per CU as the VGPRs allow
     // (UPL 16: 208 VGPRs, one per CU; UPL 8: 112, three; UPL <= 4: six)
     auto cap_of = [](int u) -> size_t { return u >= 16 ? 256 : u >= 8 ? 512 : (size_t)kCopyPipeMaxGrid; };
-    // Shape.  Up to 2 MiB: 8 units per lane and one barrier counter — few
-    // wide workgroups (16-64), because one counter's cost grows with its
+    // Shape.  Up to 1 MiB: 8 units per lane and one barrier counter — few
+    // wide workgroups (16-32), because one counter's cost grows with its
     // arrivals (at 2 MiB: 64 workgroups 2.11 us per copy, 256 4.04, 512 7.8;
     // r03_copy_pipe_ab.jsonl).  Above: the two-level barrier (8 group
-    // counters in parallel, per-group release words) with about 256
-    // workgroups, 4-16 units per lane: 8 MiB 3.2-3.4 us and 16 MiB 4.3-4.9
-    // against 3.2-3.7 / 5.0-5.2 for a launch per copy, where the one-counter
-    // pipe read 3.6-6.2 / 12-13 (r03_copy_pipe_hier.jsonl).
-    const bool big = n > ((size_t)2 << 20);
+    // counters in parallel, per-group release words) with up to 256
+    // workgroups of 4-16 units per lane: 4 MiB 2.56-2.59 us, 8 MiB 3.2-3.9,
+    // 16 MiB 4.3-6.0 against 2.9-3.0 / 3.2-4.2 / 5.0-6.8 for a launch per
+    // copy.  The one-counter form with 64+ workgroups read 3.07-3.14 at 2 MiB
+    // in three of four bench.py sweeps (2.08-2.14 in a fresh process), and
+    // 4.3-6.2 at 4-8 MiB after 1 GiB copies (r03_copy_pipe_hier.jsonl,
+    // r03_copy_pipe_state.jsonl).
+    const bool big = n > ((size_t)1 << 20);
     int upl = big ? 4 : 8;
     while (big && upl < 16 && (n16 + lanes * upl - 1) / (lanes * upl) > 256) upl *= 2;
     if (const char* v = getenv("MPX_COPY_PIPE_UPL"))   // A/B knob, read per call

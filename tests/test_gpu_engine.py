@@ -134,13 +134,13 @@ def test_copy_steps_grid_rule(ctx, monkeypatch, n, grid):
         ctx.free(dst)
 
 
-@pytest.mark.parametrize("n,grid", [((512 << 10) + 16, 17), (1 << 20, 32), ((1 << 20) + 16, 33), (2 << 20, 64),
+@pytest.mark.parametrize("n,grid", [((512 << 10) + 16, 17), (1 << 20, 32), ((1 << 20) + 16, 65), (2 << 20, 128),
                                     ((2 << 20) + 16, 129), (3 << 20, 192), (4 << 20, 256), (8 << 20, 256),
                                     ((8 << 20) + 16, 129), (16 << 20, 256)])
 def test_copy_pipe_grid_rule(ctx, n, grid):
     """The one-launch form of 512 KiB - 16 MiB (k_copy_pipe): 320-lane
-    workgroups (four copy waves + the barrier wave); up to 2 MiB 8 units per
-    lane and one barrier counter (16-64 workgroups), above it the two-level
+    workgroups (four copy waves + the barrier wave); up to 1 MiB 8 units per
+    lane and one barrier counter (16-32 workgroups), above it the two-level
     barrier with up to 256 workgroups of 4-16 units per lane.
     timing.nwg = workgroups."""
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n)
