@@ -210,8 +210,9 @@ def runtime_copy_rate(torch, nbytes: int, iters: int) -> float:
     return round(2 * nbytes / per / 1e9, 1)
 
 
-def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: int = 3) -> dict:
-    """Two ranks on GPU 0 (one host thread each): per-pair time of the loop."""
+def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: int = 3, pull: bool = False) -> dict:
+    """Two ranks on GPU 0 (one host thread each): per-pair time of the loop
+    (pull: the kernel engine's MPX_XFER_PULL form)."""
     with mpx.Context(2, engine) as c:
         bufs = []
         for r in range(2):
@@ -224,7 +225,7 @@ def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: in
             out = {}
 
             def side(r):
-                out[r] = c.xfer(mode, 1 - r, r, 1 - r, iters, bufs[r][0], bufs[r][1], nbytes)
+                out[r] = c.xfer(mode, 1 - r, r, 1 - r, iters, bufs[r][0], bufs[r][1], nbytes, pull=pull)
 
             th = [threading.Thread(target=side, args=(r,)) for r in range(2)]
             for t in th:
@@ -462,6 +463,40 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
                 mean_aggregate_GBps=round(statistics.mean(ok), 2) if len(ok) == len(per_round) else None)
 
 
+PULL_AB_ITERS = 100
+
+
+def push_vs_pull(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, nwg, stream, expect, expect_ack, errs) -> dict:
+    """Round 0's pairs at B in both directions of data movement of the
+    kernel engine ("try pull as well"): push (the
+    headline's form and tuned width) and pull (MPX_XFER_PULL: the receiver's
+    workgroups load the sender's peer-mapped tx into their own rx, same
+    width), each validated first (check mode, 3 iterations), then timed
+    unidirectional (-u 1) and full duplex (-x 1), PULL_AB_ITERS iterations;
+    GB/s per pair = bytes / the max over ranks of the loop's wall time.
+    Reported beside the headline, never chosen for it: that a pulled byte
+    crossed the link each iteration (no reuse from this GPU's caches) needs
+    the per-launch link counters of tools/node_profile.sh."""
+    g, peer = round_role(rounds, 0, rank)
+    out = {}
+    for name, pull in (("push", False), ("pull", True)):
+        for mode, label, mult in ((mpx.MODE_UNIDIR, "unidir", 1), (mpx.MODE_NONBLOCKING, "nonblocking", 2)):
+            dist.barrier()
+            before = len(errs)
+            safe_wall(c, errs, mode, g, rank, peer, 3, tx, rx, nbytes, check_payload=True, expect=expect[peer],
+                      expect_ack=expect_ack[peer], nwg=nwg, stream=stream, pull=pull)
+            dist.barrier()
+            w = safe_wall(c, errs, mode, g, rank, peer, PULL_AB_ITERS, tx, rx, nbytes, nwg=nwg, stream=stream,
+                          pull=pull)
+            if len(errs) > before:
+                w = float("inf")
+            t = torch.tensor([w], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            out[f"{name}_{label}_GBps"] = rate(mult * nbytes * PULL_AB_ITERS / 1e9, float(t[0]), 2)
+    out.update(bytes=nbytes, iters=PULL_AB_ITERS, width=push_name(nwg, stream) if nwg else "default")
+    return out
+
+
 def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
     """8 B ping-pong half round trip of every pair, round by round
     (PAIR_LATENCY_ITERS iterations each): "g1>g0" -> us, the pair's slower
@@ -637,6 +672,11 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
             out["ll_vs_bulk_half_rtt_us"] = ll_vs_bulk(mpx, torch, dist, c, rounds, rank, tx, rx, errs)
         if nbytes >= HBV3_BYTES:
             out["hbv3_rounds"] = hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs)
+        if engine == "kernel":
+            # last: a pull failure (e.g. a peer's tx not mapped) breaks only
+            # what comes after it on this context
+            out["push_vs_pull"] = push_vs_pull(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, nwg, stream,
+                                               [d[1] for d in descs], [d[2] for d in descs], errs)
         every = [None] * world
         dist.all_gather_object(every, errs[:3])
         if any(every):
@@ -792,6 +832,8 @@ def main() -> None:
             extras["loopback_pingpong_8B_half_rtt_us"] = round(lat["per_iter_us"] / 2, 3)
             uni = loopback_pair(mpx, "kernel", mpx.MODE_UNIDIR, 4 << 20, 200)
             extras["loopback_unidir_4MiB_GBps"] = round((4 << 20) / (uni["per_iter_us"] * 1e-6) / 1e9, 2)
+            uni = loopback_pair(mpx, "kernel", mpx.MODE_UNIDIR, 4 << 20, 200, pull=True)
+            extras["loopback_pull_unidir_4MiB_GBps"] = round((4 << 20) / (uni["per_iter_us"] * 1e-6) / 1e9, 2)
             extras["runtime_copy_hbm_GBps"] = runtime_copy_rate(torch, nbytes, iters)
         ceil = hbm_one_direction_ceiling()
         if ceil:
@@ -848,6 +890,8 @@ def main() -> None:
             extras["hbv3_rounds_unidir"] = res["hbv3_rounds"]
         if "ll_vs_bulk_half_rtt_us" in res:
             extras["ll_vs_bulk_half_rtt_us"] = res["ll_vs_bulk_half_rtt_us"]
+        if "push_vs_pull" in res:
+            extras["push_vs_pull"] = res["push_vs_pull"]
         if "round0_sweep" in res:
             extras["round0_sweep"] = res["round0_sweep"]
             bidir = res["round0_sweep"].get(f"nonblocking_{nbytes}")

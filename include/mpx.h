@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 4
+#define MPX_ABI_VERSION 5
 #define MPX_MAX_RANKS 64          /* ranks one context can address           */
 #define MPX_RANK_DESC_BYTES 512   /* size of the opaque exported descriptor  */
 #define MPX_RCCL_ID_BYTES 128     /* size of an RCCL unique id               */
@@ -107,7 +107,10 @@ typedef struct mpx_timing {
     int32_t protocol;         /* 0 = LL granules, 1 = bulk+flags, 2 = SDMA,
                                  3 = RCCL, 4 = local copy kernel (a launch per
                                  copy), 5 = local copy, all iterations in one
-                                 launch (k_copy_steps)                          */
+                                 launch (k_copy_steps), 6 = the same with the
+                                 next copy's loads in flight (k_copy_pipe),
+                                 7 = bulk payloads pulled by the receiver
+                                 (MPX_XFER_PULL)                                */
     int32_t check_failures;   /* iterations whose payload checksum mismatched  */
     uint64_t check_iters;     /* iterations whose payload was checksummed      */
     /* receive accounting, as the reference's loop completes receives: every
@@ -137,6 +140,15 @@ typedef struct mpx_xfer_opts {
    hint on top of their system-scope write-through policy (sc0 sc1 nt instead
    of sc0 sc1).  Visibility is unchanged, so the two sides need not agree. */
 #define MPX_XFER_STREAM 1
+/* mpx_xfer_opts.flags: kernel engine only — every B-byte payload is PULLED:
+   the sender publishes "tx holds message k" (one store into the receiver's
+   mailbox) and the receiver's kernel loads the bytes from the sender's
+   peer-mapped tx into its own rx, instead of the sender storing them into
+   the receiver's rx.  LL messages (<= the link's LL threshold) and the unidir
+   1-byte ack stay pushes.  Both sides of a link must set it alike (as nwg);
+   the SDMA and RCCL engines refuse it (MPX_ERR_UNSUPPORTED).  The environment
+   variable MPX_XFER_PULL=1 makes it the kernel engine's default. */
+#define MPX_XFER_PULL 2
 
 /* opaque context */
 typedef struct mpx_ctx mpx_ctx;

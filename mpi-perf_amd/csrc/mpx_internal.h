@@ -21,7 +21,7 @@ constexpr int kStageMaxBytes = 60 << 10; // LDS-staged tx chunk per workgroup, m
 
 // Protocol ids reported in mpx_timing.protocol
 enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4, kProtoCopySteps = 5,
-             kProtoCopyPipe = 6 };
+             kProtoCopyPipe = 6, kProtoPull = 7 };
 
 // One rank's receive mailbox, in that rank's HBM (uncached / fine-grained so a
 // poll sees stores that arrive over xGMI).  Written ONLY by the peers, polled
@@ -31,9 +31,14 @@ enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProt
 //                  system-scope store after that workgroup's payload drained)
 //   ll[s][g]     : LL granule g of the current small message from sender s:
 //                  {tag:32 | payload:32}, tag = ll_tag(seq), one 8-byte store
-//   credit[s][w] : non-blocking check mode only — sequence number of the last
-//                  of THIS rank's pushes whose chunk w rank s has checksummed
-//                  (and poisoned), i.e. the ring slot it used is free again
+//   credit[s][w] : sequence number of the last of THIS rank's pushes whose
+//                  chunk w rank s is done with: non-blocking check mode —
+//                  checksummed (and poisoned), i.e. the ring slot it used is
+//                  free again; pull mode — loaded from this rank's tx, i.e.
+//                  that chunk of tx may change again
+//   ready[s]     : pull mode (MPX_XFER_PULL) — sequence number of the last
+//                  push rank s made available in its tx (one store per send,
+//                  by the sender; the receiver loads the bytes itself)
 //   posted[s]    : "receives posted", written by rank s: the number of the
 //                  latest transfer call between s and this rank that s has
 //                  started.  It grows by one per call on both sides
@@ -49,6 +54,7 @@ struct Mailbox {
     u64 ll[MPX_MAX_RANKS][kLLGranules];
     u64 credit[MPX_MAX_RANKS][kMaxPushWG];
     u64 posted[MPX_MAX_RANKS];
+    u64 ready[MPX_MAX_RANKS];
 };
 
 // Per-rank host-mapped status words (written by the device, read by the host
@@ -68,9 +74,10 @@ struct Status {
 
 // Device scratch words of a rank (zeroed per kernel-engine call, [0..3]):
 //   [0] grid-barrier counter  [1] abort word  [2] finished workgroups
+//   [3] pull mode: chunks landed in rx this call (all receives, all workgroups)
 //   [4..5] SDMA engine's device-side sequence base {tx, rx}
 constexpr int kScratchWords = 8;
-constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrSeqBase = 4, kScrLink = 6;
+constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrLanded = 3, kScrSeqBase = 4, kScrLink = 6;
 
 // Non-blocking check mode ("ring"): receive j of a call with `iters`
 // iterations lands in slot (iters-1-j) mod S of the receiver, where slot 0 is
@@ -123,8 +130,15 @@ struct XferArgs {
                                  // are skipped (flag still published); 0 = off
     u64 call;                    // number of this call on the link (Mailbox.posted)
     int lag_wg;                  // test knob (MPX_TEST_LAG_WG): workgroup that stalls
-    u64 lag_ticks;               //   lag_ticks before checking the call's last
-                                 //   receive (non-blocking check mode); 0 = off
+    u64 lag_ticks;               //   lag_ticks before checking (non-blocking check
+                                 //   mode) or pulling (pull mode) the call's last
+                                 //   receive; 0 = off
+    // pull mode (MPX_XFER_PULL, k_xfer_pull): bulk payloads are loaded by the
+    // receiver from the sender's tx instead of stored by the sender
+    const unsigned char* peer_tx;   // the peer's tx, mapped into this process
+    int pull;                    // 1 = this call's bulk payloads are pulled
+    int no_pull_wait;            // test knob (MPX_TEST_NO_PULL_WAIT): a sending side
+                                 // ends without waiting for the peer's loads of tx
 };
 
 // LL threshold of a link.  Within one GPU the bulk path's extra hop (payload

@@ -886,6 +886,127 @@ struct Loop {
         __syncthreads();
         return !aborted();
     }
+
+    // ---- pull mode (k_xfer_pull) ---------------------------------------------
+    // Bounded one-lane poll of a word this rank's workgroup reads; `sys` =
+    // a word the peer writes (system scope), else a device-local counter.
+    template <bool SYS>
+    __device__ bool poll_ge(const u64* p, u64 want, int iter) const {
+        if (threadIdx.x == 0) {
+            const u64 t0 = now_ticks();
+            u64 spins = 0;
+            for (;;) {
+                const u64 v = SYS ? ld_sys(p) : __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (v >= want) break;
+                if (should_stop(++spins, t0)) { give_up(iter); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
+
+    // Send (workgroup 0): tx holds push `seq` — one system-scope store into
+    // the peer's ready word.  tx is read-only while the loop runs and the
+    // reference re-sends the same buffer every iteration (mpi_perf.c:74,80,
+    // 99,105,136), so no byte moves here.  `landed` > 0: first wait until
+    // that many chunks of this call's receives are in rx (a blocking Recv
+    // completes before the next Send, mpi_perf.c:75-80).
+    __device__ bool pull_send(u64 seq, u64 landed, int iter) const {
+        if (blockIdx.x != 0) return true;
+        if (landed && !poll_ge<false>(&a.gbar[kScrLanded], landed, iter)) return false;
+        if (threadIdx.x == 0) st_sys(&a.peer_mb->ready[a.my_slot], seq);
+        return true;
+    }
+
+    // This workgroup's chunk of a pull: units from the peer's tx into rx, 8
+    // loads in flight per lane.  Loads are sc0|sc1 (system scope: each
+    // iteration's bytes come from the peer's memory, not from a line this
+    // GPU cached in an earlier iteration or call); stores are sc0|sc1
+    // write-through, as a push lands, so check mode and the host read what
+    // arrived.  Units past the chunk are out of the resources' range (loads
+    // return 0, stores are dropped), so the loop has no per-unit branch.
+    __device__ void pull_units(__amdgpu_buffer_rsrc_t src, __amdgpu_buffer_rsrc_t dst, int nv) const {
+        constexpr int D = 8;
+        for (int v = threadIdx.x; v < nv; v += D * kBlock) {
+            v4u r[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j)
+                r[j] = __builtin_amdgcn_raw_buffer_load_b128(src, (unsigned)(v + j * kBlock) * 16, 0, kAuxSys);
+#pragma unroll
+            for (int j = 0; j < D; ++j)
+                __builtin_amdgcn_raw_buffer_store_b128(r[j], dst, (unsigned)(v + j * kBlock) * 16, 0, kAuxSys);
+        }
+    }
+
+    // Receive (every workgroup, grid = nwg): wait for the peer's ready word,
+    // load this workgroup's chunk of the peer's tx into rx, check it (check
+    // mode), then return the chunk to the peer (credit: its tx chunk may
+    // change again) and count it landed.
+    __device__ bool pull_recv(long long n, u64 seq, int iter) const {
+        if (!poll_ge<true>(&a.my_mb->ready[a.peer_slot], seq, iter)) return false;
+        if (a.lag_ticks && (int)blockIdx.x == a.lag_wg && iter + 1 == a.iters) {
+            // test knob (MPX_TEST_LAG_WG): this workgroup is late to load the
+            // call's last payload, so the peer's call must wait for it
+            if (threadIdx.x == 0) {
+                const u64 t0 = now_ticks();
+                while (now_ticks() - t0 < a.lag_ticks) __builtin_amdgcn_s_sleep(127);
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __syncthreads();
+        long long lo, hi;
+        chunk_of(n, &lo, &hi);
+        if (lo < hi) {
+            const unsigned bytes = (unsigned)(hi - lo);
+            const __amdgpu_buffer_rsrc_t src = rsrc(a.peer_tx + lo, bytes);
+            const __amdgpu_buffer_rsrc_t dst = rsrc(a.rx + lo, bytes);
+            const int nv = (int)(bytes >> 4);
+            if (a.skip_push != iter + 1) {             // test knob: this payload is "lost"
+                pull_units(src, dst, nv);
+                const unsigned tail = bytes & 15;
+                if (threadIdx.x < tail) {
+                    const unsigned o = (unsigned)nv * 16 + threadIdx.x;
+                    __builtin_amdgcn_raw_buffer_store_b8(__builtin_amdgcn_raw_buffer_load_b8(src, o, 0, kAuxSys), dst, o,
+                                                         0, kAuxSys);
+                }
+            }
+        }
+        drain_stores();                                // loads and stores of every wave
+        if (a.check) check(n, iter);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            st_sys(&a.peer_mb->credit[a.my_slot][blockIdx.x], seq);
+            __hip_atomic_fetch_add(&a.gbar[kScrLanded], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return true;
+    }
+
+    // Workgroup 0: every chunk of this side's sends up to `seq` was loaded
+    // by the peer (its credits), so tx may change once the call returns —
+    // MPI_Send's buffer-reuse rule, and the non-blocking loop's Waitall over
+    // the send requests (mpi_perf.c:110,122).
+    __device__ bool wait_pulled(u64 seq, int iter) const {
+        if (blockIdx.x != 0) return true;
+        if (threadIdx.x < 64) {
+            const u64* c = &a.my_mb->credit[a.peer_slot][0];
+            const u64 t0 = now_ticks();
+            u64 spins = 0;
+            for (;;) {
+                bool ok = true;
+                for (int j = threadIdx.x; j < a.nwg; j += 64) ok &= ld_sys(c + j) >= seq;
+                if (__all(ok)) break;
+                if (should_stop(++spins, t0)) {
+                    if (threadIdx.x == 0) give_up(iter);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
 };
 
 // One instantiation per (mode, side): each carries only its own loop, so
@@ -1042,6 +1163,97 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     }
 }
 
+// k_xfer_pull: the three loops with every B-byte payload PULLED by its
+// receiver (MPX_XFER_PULL; SURVEY.md §7 step 4, "try pull as well").  A send
+// is one store into the peer's ready word (Loop::pull_send); the receiver's
+// workgroups load their chunks of the sender's tx over xGMI into their own rx
+// (Loop::pull_recv).  A receive is complete once every workgroup's chunk
+// is in (the local landed counter); the sender's tx is free again once every
+// chunk's credit came back, which each sending side waits for before its
+// kernel ends.  rx is only ever written by its own rank's kernel, so no
+// payload of the next call can land before this rank's next call starts.
+// LL messages stay pushes (their data is their flag), and so does the
+// unidir 1-byte ack (mpi_perf.c:137,142).  Grid: nwg for a side that
+// receives B-byte payloads, 1 for unidir group 1 (it only publishes and
+// takes acks).
+template <int MODE, int GROUP>
+__global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
+    __shared__ int s_abort;
+    __shared__ u64 lds4[4];
+    if (threadIdx.x == 0) s_abort = 0;
+    Loop<MODE> L{a, &s_abort, lds4, nullptr, {}};
+    const long long n = a.len;
+    const u64 nw = (u64)a.nwg;
+    if (MODE == MPX_MODE_UNIDIR && GROUP == 0 && blockIdx.x == 0) L.preload_ll(1);   // the ack's byte
+    __syncthreads();
+    u64 txs = a.tx_seq0, rxs = a.rx_seq0, done = 0;
+    L.post_receives();
+    bool ok = true;
+    int inflight = 0;
+    for (int i = 0; ok && i < a.iters; ++i) {
+        if constexpr (MODE == MPX_MODE_PINGPONG) {    // mpi_perf.c:70-82
+            if constexpr (GROUP == 1) {
+                ok = L.pull_send(++txs, nw * (u64)i, i) && L.pull_recv(n, ++rxs, i);   // Send(tag 1), Recv(tag 2)
+            } else {
+                ok = L.pull_recv(n, ++rxs, i) && L.pull_send(++txs, nw * (u64)(i + 1), i);   // Recv(tag 1), Send(tag 2)
+            }
+            if (ok) ++done;
+        } else if constexpr (MODE == MPX_MODE_UNIDIR) {  // mpi_perf.c:132-144
+            if constexpr (GROUP == 1) {
+                ok = L.pull_send(++txs, 0, i) && L.recv(1, ++rxs, i);   // Send(tx, B), Recv(rx, 1)
+                if (ok) {
+                    ++done;
+                    if (a.check) L.check(1, i);
+                }
+            } else {
+                ok = L.pull_recv(n, ++rxs, i);           // Recv(rx, B)
+                if (ok) ++done;
+                // Send(tx, 1) once every chunk is in (workgroup 0's LL push)
+                if (ok && blockIdx.x == 0) ok = L.template poll_ge<false>(&a.gbar[kScrLanded], nw * (u64)(i + 1), i);
+                if (ok) L.send(1, ++txs);
+            }
+        } else {                                       // mpi_perf.c:95-124
+            ok = L.pull_send(++txs, 0, i) && L.pull_recv(n, ++rxs, i);   // Isend + Irecv, slot `inflight`
+            if (ok && inflight == kNbWindow - 1) {
+                // Waitall(255): every workgroup waits until all chunks of
+                // receives 0..i are in (so none runs into the next window
+                // ahead of the count), workgroup 0 for the peer's loads of
+                // sends 0..254 (iterations i-255 .. i-1)
+                ok = L.template poll_ge<false>(&a.gbar[kScrLanded], nw * (u64)(i + 1), i) && L.wait_pulled(txs - 1, i);
+                done += (u64)inflight;
+                inflight = 0;
+            } else {
+                ++inflight;
+            }
+        }
+    }
+    // every send of the call loaded by the peer before tx may change again
+    const bool sent_bulk = MODE != MPX_MODE_UNIDIR || GROUP == 1;
+    if (ok && sent_bulk && a.iters > 0 && !a.no_pull_wait) ok = L.wait_pulled(txs, a.iters - 1);
+    if constexpr (MODE == MPX_MODE_NONBLOCKING) {
+        // final Waitall(inflight); then workgroup 0 counts and digests the
+        // receives the reference waits for (all but slot 255 of each full
+        // window)
+        if (blockIdx.x != 0) return;
+        if (ok && a.iters > 0) ok = L.template poll_ge<false>(&a.gbar[kScrLanded], nw * (u64)a.iters, a.iters - 1);
+        if (ok) done += (u64)inflight;
+        u64 part = 0;
+        if (ok && a.check) {
+            const u64 fmix = mix64((u64)n);
+            for (int j = threadIdx.x; j < a.iters; j += kBlock)
+                if (j % kNbWindow != kNbWindow - 1)
+                    part += __hip_atomic_load(&a.csum[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ fmix;
+        }
+        const u64 s = block_sum(part, lds4);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&a.status->recv_digest, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    } else {
+        L.account_all(done, (MODE == MPX_MODE_UNIDIR && GROUP == 1) ? 1 : n);
+    }
+}
+
 // stream engines' receive accounting (launch_account)
 __global__ __launch_bounds__(kBlock) void k_account(Status* st, const u64* csum, int j0, int count, u64 fmix) {
     __shared__ u64 lds4[4];
@@ -1063,6 +1275,16 @@ __global__ __launch_bounds__(kBlock) void k_account(Status* st, const u64* csum,
 hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     void (*k)(XferArgs) = nullptr;
+    if (a.pull) {
+        switch (a.mode) {
+            case MPX_MODE_PINGPONG: k = a.group ? k_xfer_pull<MPX_MODE_PINGPONG, 1> : k_xfer_pull<MPX_MODE_PINGPONG, 0>; break;
+            case MPX_MODE_UNIDIR: k = a.group ? k_xfer_pull<MPX_MODE_UNIDIR, 1> : k_xfer_pull<MPX_MODE_UNIDIR, 0>; break;
+            case MPX_MODE_NONBLOCKING: k = k_xfer_pull<MPX_MODE_NONBLOCKING, 0>; break;   // both sides alike
+            default: return hipErrorInvalidValue;
+        }
+        hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, a);
+        return hipGetLastError();
+    }
     switch (a.mode) {
         case MPX_MODE_PINGPONG: k = a.group ? k_xfer<MPX_MODE_PINGPONG, 1> : k_xfer<MPX_MODE_PINGPONG, 0>; break;
         case MPX_MODE_UNIDIR: k = a.group ? k_xfer<MPX_MODE_UNIDIR, 1> : k_xfer<MPX_MODE_UNIDIR, 0>; break;

@@ -99,7 +99,7 @@ struct Rank {
     bool broken = false;           // a transfer timed out: link state unknown
     int dev = -1;
     char bus_id[32] = {0};
-    unsigned char* tx = nullptr;
+    unsigned char* tx = nullptr;   // local tx, or the imported rank's tx mapped here (pull mode)
     unsigned char* rx = nullptr;   // local rx, or the imported rank's rx mapped here
     size_t len = 0;
     Mailbox* mb = nullptr;         // usable from this process
@@ -134,6 +134,7 @@ struct RankDesc {
     hipIpcMemHandle_t mb_handle;
     uint64_t ring_bytes;
     hipIpcMemHandle_t ring_handle;   // valid when ring_bytes > 0
+    hipIpcMemHandle_t tx_handle;     // the rank's tx: pull mode loads from it
 };
 static_assert(sizeof(RankDesc) <= MPX_RANK_DESC_BYTES, "rank descriptor too large");
 
@@ -328,7 +329,8 @@ int skip_push_knob() {
 
 // test knob (MPX_TEST_LAG_WG="rank:wg:us"): in non-blocking check mode,
 // workgroup wg of `rank` (wg < 0 counts from the last) stalls `us`
-// microseconds before it checks the call's last receive, so that rank's call
+// microseconds before it checks the call's last receive (in pull mode: before
+// it loads the call's last payload from the peer's tx), so that rank's call
 // ends long after its peer's; read per call
 void lag_knob(int my_rank, int* wg, u64* ticks) {
     *wg = 0;
@@ -347,6 +349,14 @@ void lag_knob(int my_rank, int* wg, u64* ticks) {
 // the negative control of tests/test_gpu_ordering.py; read per call
 bool no_posted_knob() {
     const char* v = getenv("MPX_TEST_NO_POSTED");
+    return v && atoi(v) != 0;
+}
+
+// test knob (MPX_TEST_NO_PULL_WAIT=1): in pull mode a sending side's call
+// returns without waiting for the peer's loads of its tx; the negative
+// control of the pull-mode buffer-reuse test (tests/test_gpu_pull.py)
+bool no_pull_wait_knob() {
+    const char* v = getenv("MPX_TEST_NO_PULL_WAIT");
     return v && atoi(v) != 0;
 }
 
@@ -572,6 +582,17 @@ int nb_publish() {
     return k;
 }
 
+// Pull mode (MPX_XFER_PULL): the call's flag, else MPX_XFER_PULL=1 in the
+// environment (every rank of a job inherits it, so both sides agree).  Kernel
+// engine only.
+bool pull_requested(const mpx_xfer_opts* o) {
+    static const bool env_pull = [] {
+        const char* v = getenv("MPX_XFER_PULL");
+        return v && atoi(v) != 0;
+    }();
+    return (o && (o->flags & MPX_XFER_PULL)) || env_pull;
+}
+
 u64 timeout_ticks(const mpx_xfer_opts* o) {
     const u64 ms = (o && o->timeout_ms) ? o->timeout_ms : 10000;
     return ms * 100000ull;   // s_memrealtime runs at 100 MHz
@@ -587,6 +608,7 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.tx = me.tx;
     a.rx = me.rx;
     a.peer_rx = peer.rx;
+    a.peer_tx = peer.tx;
     a.my_mb = me.mb;
     a.peer_mb = peer.mb;
     a.status = me.status;
@@ -630,22 +652,29 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     a.cnt = me.cnt;
     a.slots = link_slots(me, peer, len);
     a.skip_push = skip_push_knob();
+    a.no_pull_wait = no_pull_wait_knob() ? 1 : 0;
     lag_knob(my_rank, &a.lag_wg, &a.lag_ticks);
     if (a.lag_wg < 0) a.lag_wg += a.nwg;   // -1: the last pushing workgroup
-    if (a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!me.ring || !peer.ring))
+    if (!pull_requested(o) && a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!me.ring || !peer.ring))
         return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
 
     const bool ll = mode != MPX_MODE_NONBLOCKING && len <= a.ll_max;
     const bool pushes_len = mode != MPX_MODE_UNIDIR || group == 1;
     const bool recvs_len = mode != MPX_MODE_UNIDIR || group == 0;
-    const int grid = (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;
+    // pull mode: B-byte payloads are loaded by their receiver (k_xfer_pull);
+    // LL messages stay pushes.  A receiving side runs nwg workgroups (one
+    // chunk each), unidir group 1 one (it only publishes and takes acks).
+    a.pull = (!ll && pull_requested(o)) ? 1 : 0;
+    if (a.pull && !peer.tx) return fail(MPX_ERR_STATE, "rank %d: pull mode needs rank %d's tx mapped", my_rank, peer_rank);
+    const int grid = a.pull ? (recvs_len ? a.nwg : 1)
+                            : (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;
     // bulk pushes read tx from LDS when one workgroup's chunk fits
     // (kStageMaxBytes); MPX_STAGE=0 turns it off (A/B)
     static const bool stage_on = [] {
         const char* v = getenv("MPX_STAGE");
         return !(v && atoi(v) == 0);
     }();
-    if (stage_on && !ll && pushes_len && len > 0) {
+    if (stage_on && !ll && !a.pull && pushes_len && len > 0) {
         static const long long lds_cap = [] {
             int dev = 0, per_block = 0;
             (void)hipGetDevice(&dev);
@@ -682,7 +711,7 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     t->device_s = ms * 1e-3;
     t->launches = 1;
     t->nwg = ll ? 1 : a.nwg;
-    t->protocol = ll ? kProtoLL : kProtoBulk;
+    t->protocol = ll ? kProtoLL : a.pull ? kProtoPull : kProtoBulk;
     t->recv_done = __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE);
     t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
     const unsigned err = __atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE);
@@ -1465,7 +1494,7 @@ int mpx_rank_export(mpx_ctx* ctx, int rank, void* desc) {
     const Rank& rk = ctx->r[rank];
     RankDesc d;
     memset(&d, 0, sizeof d);
-    memcpy(d.magic, "MPXRANK1", 8);
+    memcpy(d.magic, "MPXRANK2", 8);
     d.abi = MPX_ABI_VERSION;
     d.rank = rank;
     d.dev = rk.dev;
@@ -1477,6 +1506,7 @@ int mpx_rank_export(mpx_ctx* ctx, int rank, void* desc) {
     DeviceGuard g(rk.dev);
     DBG("export rank %d: rx %p mb %p (kind %d) dev %d\n", rank, (void*)rk.rx, (void*)rk.mb, rk.mb_kind, rk.dev);
     HIPCK(hipIpcGetMemHandle(&d.rx_handle, rk.rx));
+    HIPCK(hipIpcGetMemHandle(&d.tx_handle, rk.tx));
     HIPCK(hipIpcGetMemHandle(&d.mb_handle, rk.mb));
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1494,7 +1524,7 @@ int mpx_rank_import(mpx_ctx* ctx, int rank, const void* desc) {
     if (rank < 0 || rank >= ctx->nranks) return fail(MPX_ERR_INVALID, "rank %d not in [0,%d)", rank, ctx->nranks);
     RankDesc d;
     memcpy(&d, desc, sizeof d);
-    if (memcmp(d.magic, "MPXRANK1", 8) != 0 || d.abi != MPX_ABI_VERSION || d.rank != rank)
+    if (memcmp(d.magic, "MPXRANK2", 8) != 0 || d.abi != MPX_ABI_VERSION || d.rank != rank)
         return fail(MPX_ERR_INVALID, "descriptor is not an mpx rank %d descriptor", rank);
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (ctx->r[rank].local || ctx->r[rank].imported) return fail(MPX_ERR_STATE, "rank %d already registered", rank);
@@ -1515,6 +1545,18 @@ int mpx_rank_import(mpx_ctx* ctx, int rank, const void* desc) {
     HIPCK(hipIpcOpenMemHandle(&p, d.rx_handle, hipIpcMemLazyEnablePeerAccess));
     ctx->ipc_opened.push_back(p);
     rk.rx = static_cast<unsigned char*>(p);
+    // tx is mapped for pull mode only: a failure leaves it unmapped (a pull
+    // call then reports MPX_ERR_STATE) and costs the push engines nothing
+    {
+        const hipError_t e = hipIpcOpenMemHandle(&p, d.tx_handle, hipIpcMemLazyEnablePeerAccess);
+        if (e == hipSuccess) {
+            ctx->ipc_opened.push_back(p);
+            rk.tx = static_cast<unsigned char*>(p);
+        } else {
+            DBG("import rank %d: tx not mapped (%s): no pull mode with it\n", rank, hipGetErrorString(e));
+            (void)hipGetLastError();
+        }
+    }
     rk.ring_bytes = d.ring_bytes;
     if (d.ring_bytes) {
         HIPCK(hipIpcOpenMemHandle(&p, d.ring_handle, hipIpcMemLazyEnablePeerAccess));
@@ -1553,8 +1595,12 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     if ((size_t)buff_len > me.len || (!rccl && (size_t)buff_len > peer.len))
         return fail(MPX_ERR_INVALID, "buff_len %d exceeds an attached length (%zu, %zu)", buff_len, me.len, peer.len);
     const int check = opts && opts->check;
+    if (opts && (opts->flags & MPX_XFER_PULL) && ctx->engine != MPX_ENGINE_KERNEL)
+        return fail(MPX_ERR_UNSUPPORTED, "pull mode (MPX_XFER_PULL) is a kernel-engine mode");
+    const bool pull = ctx->engine == MPX_ENGINE_KERNEL && pull_requested(opts);
     if (check) TRY(ensure_csum(me, iters));
-    if (check && mode == MPX_MODE_NONBLOCKING && ctx->engine != MPX_ENGINE_RCCL) {
+    // (pull mode receives into rx in order: no receive ring)
+    if (check && !pull && mode == MPX_MODE_NONBLOCKING && ctx->engine != MPX_ENGINE_RCCL) {
         // both ends of the link, under the lock: the other rank's thread may
         // be here too, and both must see both rings before sizing the slots
         std::lock_guard<std::mutex> lk(ctx->mu);

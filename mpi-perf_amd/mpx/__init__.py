@@ -29,12 +29,13 @@ MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
 MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": MODE_UNIDIR}
 FILL_BYTE, FILL_SPLITMIX = 0, 1
 XFER_STREAM = 1
-ABI_VERSION = 4
+XFER_PULL = 2
+ABI_VERSION = 5
 PATTERN_SEED = 0x6D70695F70657266
 MAX_RANKS = 64
 RANK_DESC_BYTES = 512
 RCCL_ID_BYTES = 128
-PROTOCOLS = {0: "ll", 1: "bulk", 2: "sdma", 3: "rccl", 4: "copy", 5: "copy_steps", 6: "copy_pipe"}
+PROTOCOLS = {0: "ll", 1: "bulk", 2: "sdma", 3: "rccl", 4: "copy", 5: "copy_steps", 6: "copy_pipe", 7: "pull"}
 
 
 class Timing(C.Structure):
@@ -224,8 +225,9 @@ class Context:
 
     def xfer(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, tx: Buffer, rx: Buffer,
              length: int, check_payload: bool = False, expect: int = 0, expect_ack: int = 0,
-             timeout_ms: int = 0, nwg: int = 0, stream: bool = False) -> Timing:
-        o = XferOpts(check=1 if check_payload else 0, flags=XFER_STREAM if stream else 0, expect_checksum=expect,
+             timeout_ms: int = 0, nwg: int = 0, stream: bool = False, pull: bool = False) -> Timing:
+        flags = (XFER_STREAM if stream else 0) | (XFER_PULL if pull else 0)
+        o = XferOpts(check=1 if check_payload else 0, flags=flags, expect_checksum=expect,
                      expect_ack=expect_ack, timeout_ms=timeout_ms, nwg=nwg)
         t = Timing()
         st = self.L.mpx_xfer_ex(self.h, mode, group, my_rank, peer_rank, iters, C.c_void_p(tx.ptr),

@@ -21,6 +21,8 @@ SIZES = (1, 8, 4097, 8191, 8192, 8193, 65541, 1 << 20)
 def main():
     d, rank = sys.argv[1], int(sys.argv[2])
     engine = sys.argv[3] if len(sys.argv) > 3 else "kernel"
+    pull = engine == "kernel-pull"   # the kernel engine in pull mode (MPX_XFER_PULL)
+    engine = "kernel" if pull else engine
     # "cross": rank r on GPU r (the pair moves its bytes over xGMI); else GPU 0
     dev = rank if len(sys.argv) > 4 and sys.argv[4] == "cross" and not os.environ.get("MPX_MULTI_REHEARSE") else 0
     peer = 1 - rank
@@ -50,7 +52,7 @@ def main():
         for n in SIZES:
             iters = 300 if mode == mpx.MODE_NONBLOCKING else 9
             t = c.xfer(mode, group, rank, peer, iters, tx, rx, n, check_payload=True,
-                       expect=peer_sums[str(n)], expect_ack=peer_sums["1"], timeout_ms=5000)
+                       expect=peer_sums[str(n)], expect_ack=peer_sums["1"], timeout_ms=5000, pull=pull)
             m = 1 if (mode == mpx.MODE_UNIDIR and group == 1) else n
             results.append(dict(mode=mode, n=n, iters=iters, check_iters=t.check_iters,
                                 check_failures=t.check_failures, recv_done=t.recv_done,

@@ -1,6 +1,7 @@
 """One rank of the two-process ordering tests (tests/test_gpu_ordering.py).
 
 argv: <dir> <rank> <engine> <scenario> [mode check n iters]
+engine "kernel-pull": the kernel engine in pull mode (MPX_XFER_PULL).
 Each process owns one context with one rank on GPU 0, exports it, imports the
 other rank over IPC, runs the scenario of tests/ordering.py and writes
 <dir>/result_<rank>.json.
@@ -37,7 +38,8 @@ def main():
     peer = 1 - rank
     # MPX_ORDER_CROSS=1: rank r on GPU r (the pair spans GPUs, bytes over xGMI)
     dev = rank if os.environ.get("MPX_ORDER_CROSS") and not os.environ.get("MPX_MULTI_REHEARSE") else 0
-    c = mpx.Context(2, engine)
+    pull = engine == "kernel-pull"
+    c = mpx.Context(2, "kernel" if pull else engine)
     tx, rx, scratch = c.alloc(dev, O.CAP), c.alloc(dev, O.CAP), c.alloc(dev, O.CAP)
     sums = O.pattern_sums(c, scratch, rank, peer)
     c.fill(tx, O.CAP, mpx.FILL_SPLITMIX, O.key(rank, peer, 0))
@@ -48,10 +50,10 @@ def main():
     c.import_rank(peer, wait_for(d, f"desc_{peer}.bin"))
     peer_sums = json.loads(wait_for(d, f"sums_{peer}.json"))
     if scenario == "lag":
-        res = O.lag(c, rank, tx, rx, peer_sums)
+        res = O.lag(c, rank, tx, rx, peer_sums, pull=pull)
     else:
         mode, check, n, iters = (int(x) for x in sys.argv[5:9])
-        res = O.race(c, rank, tx, rx, peer_sums, mode, bool(check), n, iters)
+        res = O.race(c, rank, tx, rx, peer_sums, mode, bool(check), n, iters, pull=pull)
     publish(d, f"result_{rank}.json", json.dumps(res).encode())
     c.close()
 

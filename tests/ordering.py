@@ -17,6 +17,11 @@ rank 1 between two calls and changing its payload (pattern A, then B):
   the length and the push width, so its chunks and receive slots cover bytes
   the stalled workgroup still owns under call 1's layout.  Every payload of
   both calls must pass its checksum.
+
+Both run in pull mode too (`pull=True`, MPX_XFER_PULL): there the stalled
+workgroup has not yet LOADED call 1's last payload from rank 0's tx when rank 0
+would like to return and rewrite tx; rank 0's call must wait for it (MPI_Send's
+buffer-reuse rule), so the lag scenario checks the sender side's order.
 """
 from __future__ import annotations
 
@@ -55,12 +60,12 @@ def pattern_sums(c: mpx.Context, scratch: mpx.Buffer, rank: int, peer: int) -> d
     return out
 
 
-def lag(c: mpx.Context, rank: int, tx: mpx.Buffer, rx: mpx.Buffer, peer_sums: dict) -> dict:
+def lag(c: mpx.Context, rank: int, tx: mpx.Buffer, rx: mpx.Buffer, peer_sums: dict, pull: bool = False) -> dict:
     peer, group = 1 - rank, 1 if rank == 0 else 0
     res = {}
     try:
         t = c.xfer(mpx.MODE_NONBLOCKING, group, rank, peer, LAG_ITERS, tx, rx, LAG_N1, check_payload=True,
-                   expect=peer_sums[f"0:{LAG_N1}"], timeout_ms=10000)
+                   expect=peer_sums[f"0:{LAG_N1}"], timeout_ms=10000, pull=pull)
         res["call1"] = dict(ok=True, check_iters=t.check_iters, nwg=t.nwg)
     except mpx.MpxError as e:
         res["call1"] = dict(ok=False, error=str(e))
@@ -69,7 +74,7 @@ def lag(c: mpx.Context, rank: int, tx: mpx.Buffer, rx: mpx.Buffer, peer_sums: di
     it = 1 if rank == 1 else 0          # rank 1 receives rank 0's new pattern
     try:
         t = c.xfer(mpx.MODE_NONBLOCKING, group, rank, peer, LAG_ITERS, tx, rx, LAG_N2, check_payload=True,
-                   expect=peer_sums[f"{it}:{LAG_N2}"], timeout_ms=10000, nwg=LAG_NWG2)
+                   expect=peer_sums[f"{it}:{LAG_N2}"], timeout_ms=10000, nwg=LAG_NWG2, pull=pull)
         res["call2"] = dict(ok=True, check_iters=t.check_iters, nwg=t.nwg)
     except mpx.MpxError as e:
         res["call2"] = dict(ok=False, error=str(e))
@@ -77,7 +82,7 @@ def lag(c: mpx.Context, rank: int, tx: mpx.Buffer, rx: mpx.Buffer, peer_sums: di
 
 
 def race(c: mpx.Context, rank: int, tx: mpx.Buffer, rx: mpx.Buffer, peer_sums: dict, mode: int, check: bool,
-         n: int, iters: int) -> dict:
+         n: int, iters: int, pull: bool = False) -> dict:
     peer, group = 1 - rank, 1 if rank == 0 else 0
     m = 1 if (mode == mpx.MODE_UNIDIR and group == 1) else n   # what this rank receives
     res = {}
@@ -85,7 +90,7 @@ def race(c: mpx.Context, rank: int, tx: mpx.Buffer, rx: mpx.Buffer, peer_sums: d
         it = 1 if (rank == 1 and call == 2) else 0
         try:
             c.xfer(mode, group, rank, peer, iters, tx, rx, n, check_payload=check, expect=peer_sums[f"{it}:{n}"],
-                   expect_ack=peer_sums["0:1"], timeout_ms=10000)
+                   expect_ack=peer_sums["0:1"], timeout_ms=10000, pull=pull)
             res[f"call{call}"] = dict(ok=True)
         except mpx.MpxError as e:
             res[f"call{call}"] = dict(ok=False, error=str(e))

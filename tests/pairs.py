@@ -61,7 +61,7 @@ class Pairs:
         tx = self.bufs[self.peer(r)][0]
         return self.c.checksum(tx, n), self.c.checksum(tx, 1)
 
-    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0, stream=False):
+    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0, stream=False, pull=False):
         ranks = list(range(2 * self.np)) if ranks is None else ranks
         exp = {r: self.expect(r, n) for r in ranks}
         out, errs = {}, {}
@@ -70,7 +70,7 @@ class Pairs:
             try:
                 out[r] = self.c.xfer(mode, self.group(r), r, self.peer(r), iters, self.bufs[r][0], self.bufs[r][1],
                                      n, check_payload=check, expect=exp[r][0], expect_ack=exp[r][1],
-                                     timeout_ms=timeout_ms, nwg=nwg, stream=stream)
+                                     timeout_ms=timeout_ms, nwg=nwg, stream=stream, pull=pull)
             except mpx.MpxError as e:
                 errs[r] = e
 

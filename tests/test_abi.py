@@ -28,7 +28,9 @@ def test_every_header_symbol_is_exported():
 
 def test_version_and_strerror():
     L = mpx.lib()
-    assert L.mpx_version() == 4   # 2: recv_done / recv_digest; 3: 64 ranks per context; 4: receive-posted mailbox word
+    # 2: recv_done / recv_digest; 3: 64 ranks per context; 4: receive-posted mailbox word;
+    # 5: pull mode (MPX_XFER_PULL, tx in the rank descriptor)
+    assert L.mpx_version() == 5
     texts = {L.mpx_strerror(i).decode() for i in range(9)}
     assert len(texts) == 9
     assert L.mpx_strerror(12345) == b"unknown mpx status"
@@ -56,3 +58,6 @@ def test_header_constants_match_binding():
     assert "#define MPX_RANK_DESC_BYTES 512" in txt
     assert "0x6d70695f70657266ULL" in txt and mpx.PATTERN_SEED == 0x6D70695F70657266
     assert "#define MPX_LINK_XGMI 4" in txt and mpx.LINK_TYPES[4] == "xgmi"
+    assert f"#define MPX_ABI_VERSION {mpx.ABI_VERSION}" in txt
+    assert f"#define MPX_XFER_STREAM {mpx.XFER_STREAM}" in txt
+    assert f"#define MPX_XFER_PULL {mpx.XFER_PULL}" in txt and mpx.PROTOCOLS[7] == "pull"

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "kernel-pull"])
 def test_two_process_ipc_pair(tmp_path, engine):
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "ipc_worker.py"), str(tmp_path), str(r), engine],
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in (0, 1)]
@@ -34,3 +34,6 @@ def test_two_process_ipc_pair(tmp_path, engine):
             # (receive slots in the peer's IPC-mapped ring)
             assert x["check_failures"] == 0 and x["check_iters"] == x["iters"], (r, x)
             assert x["recv_done"] == (x["iters"] - x["iters"] // 256 if x["mode"] == 1 else x["iters"]), (r, x)
+            if engine == "kernel-pull":   # B-byte payloads pulled (protocol 7) above the 2 KiB LL threshold
+                ll = x["mode"] != 1 and x["n"] <= 2048
+                assert x["protocol"] == (0 if ll else 7), (r, x)

@@ -117,6 +117,40 @@ def test_lagging_workgroup_layout_change_processes(tmp_path):
     assert_lag_ok(run_processes(tmp_path, "kernel", ["lag"], O.lag_env()))
 
 
+# ---- pull mode (MPX_XFER_PULL): the sender's call waits for the peer's loads -
+def test_pull_lagging_receiver_keeps_the_senders_tx_threads(monkeypatch):
+    """Rank 1's last workgroup stalls before loading call 1's last payload;
+    rank 0 rewrites tx as soon as its call 1 returns.  Every payload of both
+    calls must still pass: rank 0's call returns only after rank 1's loads."""
+    for k, v in O.lag_env().items():
+        monkeypatch.setenv(k, v)
+    assert_lag_ok(run_threads(lambda c, r, tx, rx, s: O.lag(c, r, tx, rx, s, pull=True)))
+
+
+def test_pull_lagging_receiver_keeps_the_senders_tx_processes(tmp_path):
+    assert_lag_ok(run_processes(tmp_path, "kernel-pull", ["lag"], O.lag_env()))
+
+
+def test_pull_lagging_receiver_fails_without_the_wait(monkeypatch):
+    """Negative control: MPX_TEST_NO_PULL_WAIT=1 lets rank 0's call return
+    before rank 1's stalled workgroup loaded its chunk; rank 0's new tx then
+    lands in call 1's last payload and rank 1's check reports it."""
+    for k, v in O.lag_env().items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("MPX_TEST_NO_PULL_WAIT", "1")
+    out = run_threads(lambda c, r, tx, rx, s: O.lag(c, r, tx, rx, s, pull=True))
+    assert not out[1]["call1"]["ok"] and "failed the checksum" in out[1]["call1"]["error"], out
+
+
+@pytest.mark.parametrize("check", [False, True])
+@pytest.mark.parametrize("mode", list(MODES))
+def test_pull_rx_read_between_calls_threads(mode, check):
+    n, iters = RACE_CASES[0]
+    it = 300 if mode == "nonblocking" else iters
+    out = run_threads(lambda c, r, tx, rx, s: O.race(c, r, tx, rx, s, MODES[mode], check, n, it, pull=True))
+    assert_race_ok(out)
+
+
 @pytest.mark.parametrize("n,iters", RACE_CASES)
 @pytest.mark.parametrize("check", [False, True])
 @pytest.mark.parametrize("mode", list(MODES))
