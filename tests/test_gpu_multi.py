@@ -87,19 +87,21 @@ CFG3_SIZES = [0, 1, 8, 4097, 8191, 8192, 8193, 65541, 456131, 4 << 20]
 
 
 @pytest.mark.parametrize("mode", list(MODES))
-@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("engine", ENGINES + ["kernel-pull"])
 def test_cfg3_cross_gpu_pair_every_payload(engine, mode):
     """GPU 0 (group 1) <-> GPU 1 (group 0), threads of one process: every
     size around the cross-GPU LL threshold and up to 4 MiB, every payload
-    checksummed on the receiver (reads of bytes the peer wrote over xGMI),
-    receives counted on the device, final rx = the peer's tx."""
+    checksummed on the receiver (reads of bytes the peer wrote over xGMI, or
+    in pull mode that the receiver loaded over xGMI), receives counted on the
+    device, final rx = the peer's tx."""
     need(2, engine)
-    P = Pairs(engine, 1, 4 << 20, fill="seeded", devs=cross_gpu_devs(2))
+    pull = engine == "kernel-pull"
+    P = Pairs("kernel" if pull else engine, 1, 4 << 20, fill="seeded", devs=cross_gpu_devs(2))
     m = MODES[mode]
     try:
         for n in CFG3_SIZES:
             iters = 300 if m == mpx.MODE_NONBLOCKING else 9
-            out, errs = P.run(m, n, iters)
+            out, errs = P.run(m, n, iters, pull=pull)
             assert not errs, (n, errs)
             for r in (0, 1):
                 t = out[r]
@@ -107,8 +109,8 @@ def test_cfg3_cross_gpu_pair_every_payload(engine, mode):
                 assert t.recv_done == (iters - iters // 256 if m == mpx.MODE_NONBLOCKING else iters), (n, r)
                 k = 1 if (m == mpx.MODE_UNIDIR and r == 0) else n
                 assert P.c.checksum(P.bufs[r][1], k) == P.c.checksum(P.bufs[P.peer(r)][0], k), (n, r)
-                if engine == "kernel":    # LL up to 8 KiB across GPUs (ll_max_bytes), bulk above
-                    assert t.protocol == (0 if m != mpx.MODE_NONBLOCKING and n <= 8192 else 1), (n, r)
+                if engine.startswith("kernel"):   # LL up to 8 KiB across GPUs (ll_max_bytes), bulk above
+                    assert t.protocol == (0 if m != mpx.MODE_NONBLOCKING and n <= 8192 else 7 if pull else 1), (n, r)
     finally:
         P.close()
 
@@ -190,7 +192,7 @@ def _receive_digest_across_gpus(name, engine, cfg):
         P.close()
 
 
-@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "kernel-pull"])
 def test_cfg3_cross_gpu_two_processes_ipc(tmp_path, engine):
     """Two processes, rank r on GPU r, each mapping the other's rx, ring and
     mailbox through IPC (bench.py's one-process-per-GPU path)."""
@@ -239,6 +241,16 @@ def test_cfg3_lagging_workgroup_layout_change_across_gpus(tmp_path):
     T.assert_lag_ok(T.run_processes(tmp_path, "kernel", ["lag"], OR.lag_env(), cross=True))
 
 
+def test_cfg3_pull_lagging_receiver_keeps_the_senders_tx_across_gpus(tmp_path):
+    """Pull mode's buffer-reuse order across xGMI, two processes: a receiver
+    workgroup late to load call 1's last payload from the other GPU's tx;
+    the sender's call must not return (and rewrite tx) before that load."""
+    need(2)
+    import ordering as OR
+    import test_gpu_ordering as T
+    T.assert_lag_ok(T.run_processes(tmp_path, "kernel-pull", ["lag"], OR.lag_env(), cross=True))
+
+
 def test_cfg3_8B_half_rtt_reported_against_3us_target(record_property):
     """Ping-pong 8 B across GPUs (SURVEY §8d cfg3, 10^5 iterations): the half
     round trip, reported beside north_star's target (< 3 us device-initiated)
@@ -280,6 +292,17 @@ def test_cfg3_unidir_4MiB_reported_against_85pct_link_target(record_property):
         report_target(record_property, "cfg3_unidir_4MiB_frac_of_bidirectional_link", gbps / XGMI_BIDIR_GBPS, "",
                       f">= {TARGET_LINK_FRAC} of {XGMI_BIDIR_GBPS} GB/s", gbps >= TARGET_LINK_FRAC * XGMI_BIDIR_GBPS)
         assert gbps > 1
+        # the same loop pulled (MPX_XFER_PULL: G0 loads G1's tx over the
+        # link), every payload checked first; reported beside the push
+        out, errs = P.run(mpx.MODE_UNIDIR, n, 3, pull=True)
+        assert not errs, errs
+        out, errs = P.run(mpx.MODE_UNIDIR, n, iters, check=False, pull=True)
+        assert not errs, errs
+        pull_gbps = n * iters / out[0].device_s / 1e9
+        report_target(record_property, "cfg3_pull_unidir_4MiB_GBps", pull_gbps, "GB/s",
+                      f">= {TARGET_LINK_FRAC} x {XGMI_ONE_DIRECTION_GBPS} (one direction)",
+                      pull_gbps >= TARGET_LINK_FRAC * XGMI_ONE_DIRECTION_GBPS)
+        assert pull_gbps > 1
     finally:
         P.close()
 
