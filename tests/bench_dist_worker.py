@@ -88,7 +88,7 @@ class FakeMpx:
             FakeMpx.log.append(["rccl_init", r, n])
 
         def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,
-                 timeout_ms=0, nwg=0, stream=False):
+                 timeout_ms=0, nwg=0, stream=False, pull=False):
             if check_payload and self.engine == "kernel" and scenario == "kernel_fails_validation" and rank == 0:
                 raise FakeError("payload checksum mismatch")
             if (scenario == "kernel_step_fails" and self.engine == "kernel" and rank == 1 and mode == 2 and
@@ -97,7 +97,7 @@ class FakeMpx:
             if scenario == "latency_fails" and rank == 1 and mode == 0 and n == 8:
                 raise FakeError("device-side wait timed out (LL ping-pong)")
             FakeMpx.log.append(["xfer", self.engine, mode, group, me, peer, iters, n, bool(check_payload), expect,
-                                expect_ack, nwg, stream, os.environ.get("MPX_LL_MAX")])
+                                expect_ack, nwg, stream, os.environ.get("MPX_LL_MAX"), pull])
             time.sleep(0.002)
             if nwg and not check_payload and iters == 40:
                 # push tuning: rank 0 is fastest at 32, rank 1 slow at 32; the

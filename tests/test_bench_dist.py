@@ -15,6 +15,8 @@ import sys
 
 import pytest
 
+import bench
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "mpi-perf_amd"))
 from mpx.schedule import all_pairs_rounds, round_role  # noqa: E402
@@ -57,7 +59,9 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         checked = [x for x in xf if x[8] and x[2] == 2]
         timed = [x for x in xf if not x[8] and x[2] == 2][:warmup + steps]
         # validation: one checked transfer per round, against the PEER's tx
-        assert len(checked) == world - 1
+        # (then, after the headline, push_vs_pull's two checked unidir loops)
+        assert len(checked) == world - 1 + 2
+        checked = checked[:world - 1]
         for rd, x in enumerate(checked):
             g, peer = round_role(rounds, rd, r)
             assert (x[3], x[4], x[5], x[6], x[7]) == (g, r, peer, 3, n)
@@ -108,6 +112,17 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         assert all((x[3], x[5], x[6]) == (g, peer, 2000) for x in llab)
         assert set(d["res"]["ll_vs_bulk_half_rtt_us"]) == {f"{p}_{m}" for m in (1024, 4096, 8192) for p in ("ll", "bulk")}
         assert d["ll_max_after"] is None                     # the worker's environment is restored
+        # last: push against pull on round 0 at B, each validated (check
+        # mode, the peer's expected checksum) before it is timed
+        pv = [x for x in d["log"] if x[0] == "xfer" and x[7] == n and x[6] in (3, bench.PULL_AB_ITERS)][-8:]
+        assert [(x[14], x[2], x[8], x[6]) for x in pv] == [
+            (p, m, chk, it) for p in (False, True) for m in (2, 1) for chk, it in ((True, 3), (False, 100))]
+        assert all((x[3], x[5]) == (g, peer) for x in pv)
+        assert all(x[9] == (key(peer) * 31 + n) & 0xFFFFFFFFFFFFFFFF for x in pv if x[8])
+        assert all(v is not None for v in d["res"]["push_vs_pull"].values())
+        assert set(d["res"]["push_vs_pull"]) >= {f"{p}_{m}_GBps" for p in ("push", "pull")
+                                                  for m in ("unidir", "nonblocking")}
+        assert "extras_errors" not in d["res"], d["res"].get("extras_errors")
 
 
 def test_ipc_failure_on_one_rank_falls_back_to_rccl_on_every_rank(tmp_path):
