@@ -9,6 +9,11 @@
 #           link traffic is (WRREQ - WRREQ_DRAM) x 64 B per dispatch
 #   pass 3  --pmc TCC_EA0_WRREQ_WRITE_GMI_32B_sum TCC_EA0_WRREQ_WRITE_IO_32B_sum:
 #           which fabric path the non-DRAM writes take (32-B units)
+#   pass 4/5 the same timed steps in pull mode (MPX_XFER_PULL=1: the
+#           receiver, k_xfer_pull<2, 0>, loads the sender's tx): kernel trace,
+#           then --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum
+#           TCC_EA0_RDREQ_GMI_32B_sum — a pulling receiver's link reads per
+#           launch against B x iters (does every iteration cross the link?)
 # then tools/node_profile_summary.py writes gpurun_out/node_prof_n$N/summary.json.
 #
 #   N=8 tools/node_profile.sh                 on an 8-GPU node (one rank per GPU)
@@ -21,6 +26,11 @@ N=${N:-2}
 O=gpurun_out/node_prof_n$N
 mkdir -p $O
 export TMPDIR=/tmp WORLD_SIZE=$N MASTER_ADDR=127.0.0.1
+# round 2's exit order (drain, 50 ms, destroy the pooled streams in libmpx's
+# exit handler, before the profiler's): under rocprofv3 --pmc the default
+# (streams left to the runtime's teardown) segfaults in __cxa_finalize after
+# the profiler wrote its output (tools/gpu_pmc_pull.sh, round 3)
+export MPX_POOL_EXIT=sleep
 STEPS=${STEPS:-$((2 * (N - 1)))}
 run_pass() {   # pass-name, rocprofv3 options...
     local pass=$1; shift
@@ -28,7 +38,7 @@ run_pass() {   # pass-name, rocprofv3 options...
     local pids=() r
     for r in $(seq 0 $((N - 1))); do
         local prof=("$@")
-        if [ -n "$MPX_BENCH_ONE_GPU" ] && [ "$pass" != trace ] && [ $r -gt 0 ]; then prof=(); fi
+        if [ -n "$MPX_BENCH_ONE_GPU" ] && [ "${pass%trace}" = "$pass" ] && [ $r -gt 0 ]; then prof=(); fi
         if [ ${#prof[@]} -gt 0 ]; then
             RANK=$r LOCAL_RANK=$r timeout -k 10 300 rocprofv3 "${prof[@]}" --output-format csv -d $O/$pass -o rank$r \
                 -- python3 -u bench.py --gpus $N --steps $STEPS --warmup 1 --no-extras \
@@ -47,4 +57,6 @@ run_pass() {   # pass-name, rocprofv3 options...
 run_pass trace --kernel-trace --stats &&
 run_pass pmc --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum &&
 run_pass fabric --pmc TCC_EA0_WRREQ_WRITE_GMI_32B_sum TCC_EA0_WRREQ_WRITE_IO_32B_sum &&
+MPX_XFER_PULL=1 run_pass pull_trace --kernel-trace --stats &&
+MPX_XFER_PULL=1 run_pass pull_fabric --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_GMI_32B_sum &&
 python3 tools/node_profile_summary.py $O $N

@@ -20,6 +20,15 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 from mpx.schedule import all_pairs_rounds, round_role  # noqa: E402
 
 SENDER = "k_xfer<2, 1>"
+PULLER = "k_xfer_pull<2, 0>"   # pull passes: the receiver moves the bytes
+
+
+def per_dispatch(path, kernel):
+    per = {}
+    for x in csv.DictReader(open(path)):
+        if kernel in x["Kernel_Name"]:
+            per.setdefault(int(x["Dispatch_Id"]), {})[x["Counter_Name"]] = float(x["Counter_Value"])
+    return per
 
 
 def bench_line(path):
@@ -79,6 +88,31 @@ def main():
                     statistics.median(v.get("TCC_EA0_WRREQ_WRITE_GMI_32B_sum", 0) for v in last) * 32)
                 rec["io_write_bytes_per_launch"] = round(
                     statistics.median(v.get("TCC_EA0_WRREQ_WRITE_IO_32B_sum", 0) for v in last) * 32)
+        # pull passes: this rank's timed RECEIVER launches (rounds where it is
+        # group 0) load the peer's tx over the link
+        kp = sum(1 for s in range(steps) if round_role(rounds, s % (n - 1), r)[0] == 0)
+        tr = glob.glob(os.path.join(out_dir, "pull_trace", f"rank{r}_kernel_trace.csv"))
+        if tr and kp:
+            rows = [x for x in csv.DictReader(open(tr[0])) if PULLER in x["Kernel_Name"]]
+            rows.sort(key=lambda x: int(x["Start_Timestamp"]))
+            d = [(int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) * 1e-9 for x in rows[-kp:]]
+            if d:
+                rec["pull_avg_launch_us"] = round(statistics.mean(d) * 1e6, 2)
+                rec["pull_algorithmic_GBps"] = round(B * iters / statistics.mean(d) / 1e9, 2)
+        pf = glob.glob(os.path.join(out_dir, "pull_fabric", f"rank{r}_counter_collection.csv"))
+        if pf and kp:
+            per = per_dispatch(pf[0], PULLER)
+            last = [per[i] for i in sorted(per)[-kp:]]
+            if last:
+                rd = statistics.median(v.get("TCC_EA0_RDREQ_sum", 0) for v in last)
+                dram = statistics.median(v.get("TCC_EA0_RDREQ_DRAM_sum", 0) for v in last)
+                gmi = statistics.median(v.get("TCC_EA0_RDREQ_GMI_32B_sum", 0) for v in last)
+                rec["pull_gmi_read_bytes_per_launch"] = round(gmi * 32)
+                rec["pull_read_requests_per_launch"] = round(rd)
+                rec["pull_dram_read_requests_per_launch"] = round(dram)
+                rec["pull_gmi_over_algorithmic"] = round(gmi * 32 / (B * iters), 4)
+                if "pull_avg_launch_us" in rec:
+                    rec["pull_achieved_link_GBps"] = round(gmi * 32 / (rec["pull_avg_launch_us"] * 1e-6) / 1e9, 2)
         ranks.append(rec)
     doc = dict(n=n, bytes=B, iters_per_step=iters, steps=steps, kernel=SENDER,
                source="tools/node_profile.sh: rocprofv3 --kernel-trace --stats, then --pmc TCC_EA0_WRREQ_sum "

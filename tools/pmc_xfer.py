@@ -6,8 +6,11 @@ one launch moves `iters` pushes of B bytes (DESIGN.md §7 "Counter evidence").
       kernel (k_xfer<1,0>, or k_xfer_nbcheck with check) — nothing for the
       profiler's dispatch serialisation to deadlock.  variant: nb (bulk, LDS-
       staged tx), nb_hbm (bulk, tx read from HBM: MPX_STAGE=0 set by the
-      caller), nbcheck (bulk + every payload checksummed and poisoned).
-  pair <dir> <rank> <mode> <B> <iters> <check>
+      caller), nbcheck (bulk + every payload checksummed and poisoned),
+      nbpull / nbpullcheck (pull mode, MPX_XFER_PULL: k_xfer_pull loads its
+      own tx every iteration — whether each iteration's bytes come from
+      memory or from the L2 is what FETCH_SIZE shows).
+  pair <dir> <rank> <mode> <B> <iters> <check> [pull]
       rank 0 or 1 of a loopback pair in two processes (IPC, like
       tests/ipc_worker.py); only rank 0 runs under the profiler, so its
       dispatch window spans the whole co-running loop and the device-wide
@@ -35,15 +38,16 @@ def self_pair(variant, B, iters):
         c.fill(tx, B, mpx.FILL_SPLITMIX, 99)
         c.attach(0, 0, tx, rx, max(B, 1))
         want = c.checksum(tx, B)
-        check = variant == "nbcheck"
+        check = variant in ("nbcheck", "nbpullcheck")
+        pull = variant.startswith("nbpull")
         for _ in range(3):
-            t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, B, check_payload=check, expect=want)
+            t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, B, check_payload=check, expect=want, pull=pull)
         assert c.checksum(rx, B) == want
         print(json.dumps(dict(variant=variant, bytes=B, iters=iters, nwg=t.nwg, protocol=mpx.PROTOCOLS[t.protocol],
                               us_per_push=round(t.device_s / iters * 1e6, 3), check_iters=t.check_iters)))
 
 
-def pair(d, rank, mode, B, iters, check):
+def pair(d, rank, mode, B, iters, check, pull=False):
     peer = 1 - rank
     cap = max(B, 1)
     c = mpx.Context(2, "kernel")
@@ -66,7 +70,7 @@ def pair(d, rank, mode, B, iters, check):
     group = 1 if rank == 0 else 0
     for _ in range(3):
         t = c.xfer(MODES[mode], group, rank, peer, iters, tx, rx, B, check_payload=check, expect=peer_sums[0],
-                   expect_ack=peer_sums[1], timeout_ms=20000)
+                   expect_ack=peer_sums[1], timeout_ms=20000, pull=pull)
     print(json.dumps(dict(mode=mode, rank=rank, bytes=B, iters=iters, check=check,
                           protocol=mpx.PROTOCOLS[t.protocol], nwg=t.nwg,
                           us_per_iter=round(t.device_s / iters * 1e6, 3), check_iters=t.check_iters)))
@@ -77,4 +81,5 @@ if __name__ == "__main__":
     if sys.argv[1] == "self":
         self_pair(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
     else:
-        pair(sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), sys.argv[7] == "1")
+        pair(sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), sys.argv[7] == "1",
+             len(sys.argv) > 8 and sys.argv[8] == "pull")
