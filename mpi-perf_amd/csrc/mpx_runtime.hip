@@ -522,6 +522,13 @@ void destroy_stream_pool() {
     // failure: MPX_CHECK flushes stdio and _exits (host/mpx_perf.c,
     // integration/mpx_binding.c).
     const char* mode = getenv("MPX_POOL_EXIT");
+    // Under rocprofv3 --pmc (it sets ROCPROF_COUNTERS) the runtime's own
+    // teardown of streams left to it runs after the profiler's tool has
+    // finalized and segfaults in __cxa_finalize, after the counters were
+    // written (round 3, tools/gpu_pmc_pull.sh's first pass; --kernel-trace
+    // runs exit cleanly).  There the default is round 2's order: drain,
+    // 50 ms, destroy here — this handler runs before the tool's.
+    if ((!mode || !*mode) && getenv("ROCPROF_COUNTERS")) mode = "sleep";
     if (!mode || !*mode || !strcmp(mode, "keep") || p.live_contexts != 0 || p.all.empty()) return;
     if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] exit: destroying %zu pooled rank streams\n", p.all.size());
     int prev = -1;
