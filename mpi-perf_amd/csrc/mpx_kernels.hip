@@ -945,6 +945,12 @@ struct Loop {
     // change again) and count it landed.
     __device__ bool pull_recv(long long n, u64 seq, int iter) const {
         if (!poll_ge<true>(&a.my_mb->ready[a.peer_slot], seq, iter)) return false;
+        // system-scope acquire (buffer_inv sc0 sc1: the L2's lines of
+        // non-local memory, i.e. a peer GPU's tx, are dropped, so every
+        // iteration's loads cross the link), completed before any wave loads
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        drain_stores();
+        __syncthreads();
         if (a.lag_ticks && (int)blockIdx.x == a.lag_wg && iter + 1 == a.iters) {
             // test knob (MPX_TEST_LAG_WG): this workgroup is late to load the
             // call's last payload, so the peer's call must wait for it
@@ -954,8 +960,6 @@ struct Loop {
             }
             __syncthreads();
         }
-        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        __syncthreads();
         long long lo, hi;
         chunk_of(n, &lo, &hi);
         if (lo < hi) {
