@@ -493,7 +493,19 @@ def push_vs_pull(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, nwg, stream,
             t = torch.tensor([w], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             out[f"{name}_{label}_GBps"] = rate(mult * nbytes * PULL_AB_ITERS / 1e9, float(t[0]), 2)
-    out.update(bytes=nbytes, iters=PULL_AB_ITERS, width=push_name(nwg, stream) if nwg else "default")
+    # the pull's own width: unidir at every tuning width (the push's choice
+    # need not be the pull's)
+    by_width = {}
+    for w in sorted({x for x, _ in PUSH_CANDIDATES}):
+        if w * 16 > nbytes:
+            continue
+        dist.barrier()
+        wall = safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, PULL_AB_ITERS, tx, rx, nbytes, nwg=w, pull=True)
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        by_width[str(w)] = rate(nbytes * PULL_AB_ITERS / 1e9, float(t[0]), 2)
+    out.update(pull_unidir_GBps_by_width=by_width, bytes=nbytes, iters=PULL_AB_ITERS,
+               width=push_name(nwg, stream) if nwg else "default")
     return out
 
 

@@ -114,12 +114,16 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         assert d["ll_max_after"] is None                     # the worker's environment is restored
         # last: push against pull on round 0 at B, each validated (check
         # mode, the peer's expected checksum) before it is timed
-        pv = [x for x in d["log"] if x[0] == "xfer" and x[7] == n and x[6] in (3, bench.PULL_AB_ITERS)][-8:]
+        byw = [x for x in d["log"] if x[0] == "xfer" and x[14] and x[7] == n][-5:]
+        assert [(x[2], x[11], x[8]) for x in byw] == [(2, w, False) for w in (16, 32, 64, 128, 256)]
+        assert set(d["res"]["push_vs_pull"]["pull_unidir_GBps_by_width"]) == {"16", "32", "64", "128", "256"}
+        pv = [x for x in d["log"] if x[0] == "xfer" and x[7] == n and x[6] in (3, bench.PULL_AB_ITERS)][-13:-5]
         assert [(x[14], x[2], x[8], x[6]) for x in pv] == [
             (p, m, chk, it) for p in (False, True) for m in (2, 1) for chk, it in ((True, 3), (False, 100))]
         assert all((x[3], x[5]) == (g, peer) for x in pv)
         assert all(x[9] == (key(peer) * 31 + n) & 0xFFFFFFFFFFFFFFFF for x in pv if x[8])
         assert all(v is not None for v in d["res"]["push_vs_pull"].values())
+        assert all(v is not None for v in d["res"]["push_vs_pull"]["pull_unidir_GBps_by_width"].values())
         assert set(d["res"]["push_vs_pull"]) >= {f"{p}_{m}_GBps" for p in ("push", "pull")
                                                   for m in ("unidir", "nonblocking")}
         assert "extras_errors" not in d["res"], d["res"].get("extras_errors")
