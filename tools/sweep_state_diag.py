@@ -21,8 +21,30 @@ def rows(sw):
     return {k: (v["us"], v["path"]) for k, v in sw.items() if (256 << 10) <= int(k) <= (8 << 20)}
 
 
+def one_mib_arms(c, src, dst):
+    """`onemib`: which form 1 MiB should take inside bench.py — after the
+    headline's load, three interleaved rounds of the sweep to 4 MiB with 1 MiB
+    as the one-counter pipe (default), as k_copy_steps (MPX_COPY_PIPE_MIN =
+    1 MiB) and as the two-level pipe (MPX_COPY_PIPE_HIER=1)."""
+    arms = (("pipe_one_counter", {}), ("steps", {"MPX_COPY_PIPE_MIN": str(1 << 20)}),
+            ("pipe_two_level", {"MPX_COPY_PIPE_HIER": "1"}))
+    for _ in range(23):
+        c.copy(0, dst, src, G, 10)
+    for rnd in range(3):
+        for name, env in arms:
+            os.environ.update(env)
+            sw = rows(bench.copy_sweep(mpx, c, src, dst, 4 << 20))
+            for k in env:
+                os.environ.pop(k)
+            print(json.dumps(dict(state=f"after the headline load, round {rnd}", arm=name, sweep=sw)), flush=True)
+
+
 with mpx.Context(1) as c:
     src, dst = c.alloc(0, G), c.alloc(0, G)
+    if len(sys.argv) > 1 and sys.argv[1] == "onemib":
+        c.fill(src, G, mpx.FILL_SPLITMIX, 9)
+        one_mib_arms(c, src, dst)
+        sys.exit(0)
     c.fill(src, G, mpx.FILL_SPLITMIX, 9)
     t0 = time.time()
     for _ in range(23):
