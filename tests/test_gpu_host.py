@@ -20,14 +20,14 @@ PERF = os.path.join(ROOT, "mpi-perf_amd", "bin", "mpx_perf")
 GOLDEN = {c["name"]: c for c in O.golden()["cases"]}
 
 
-def run(tmp_path, args, lines=("vm",), names="vm,runsc", gpus="0,0"):
+def run(tmp_path, args, lines=("vm",), names="vm,runsc", gpus="0,0", env_extra=None):
     g1 = tmp_path / "group1"
     g1.write_text("".join(x + "\n" for x in lines))
     logs = tmp_path / "logs"
     argv = [a.replace("@G1", str(g1)).replace("@LOGS", str(logs)) for a in args]
     # MPX_HOSTNAME=localhost: the ranks' host IPv4 is 127.0.0.1, as in the
     # golden runs, so whole record lines compare (mpi_perf.c:236-237,551-554)
-    env = dict(os.environ, MPX_PROCESSOR_NAMES=names, MPX_HOSTNAME="localhost")
+    env = dict(os.environ, MPX_PROCESSOR_NAMES=names, MPX_HOSTNAME="localhost", **(env_extra or {}))
     p = run_bounded([PERF, "-g", gpus, "-t", "5000"] + argv, env=env)
     recs = []
     for f in sorted(glob.glob(str(logs / "tcp-*.log"))):
@@ -117,6 +117,19 @@ def test_engines_sdma(tmp_path):
                                    "-b", "1048576", "-c", "1", "-l", "@LOGS"])
     assert p.returncode == 0, p.stderr[-600:]
     assert len(recs) == 2 and all(f[13] == "sdma" for f in side)
+
+
+@pytest.mark.parametrize("mode_args", [[], ["-x", "1"], ["-u", "1"]])
+def test_kernel_engine_pull_mode_from_the_environment(tmp_path, mode_args):
+    """MPX_XFER_PULL=1 (how mpx_perf and the reference-side binding select
+    pull mode): the kernel engine's B-byte payloads are loaded by their
+    receivers; every payload checked, the side file names the protocol."""
+    p, recs, side = run(tmp_path, ["-w", "2", "-f", "@G1", "-n", "1", "-p", "1", "-r", "3", "-i", "20",
+                                   "-b", "1048576", "-c", "1", "-l", "@LOGS"] + mode_args,
+                        env_extra={"MPX_XFER_PULL": "1"})
+    assert p.returncode == 0, p.stderr[-600:]
+    assert len(recs) == 2
+    assert all(f[13] == "pull" and int(f[16]) == 0 and int(f[15]) == 20 for f in side), side
 
 
 def test_unidir_without_ppn_raises_sigfpe_like_reference(tmp_path):
