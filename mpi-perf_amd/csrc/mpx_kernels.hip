@@ -458,6 +458,7 @@ struct Loop {
     // every iteration, mpi_perf.c:72,80,135), so a send is stores only — no
     // tx load on the latency path.
     u64 pre[kLLUnitsPerLane];
+    u64* s_seen = nullptr;   // LDS, pull mode: the peer's ready word as last read
 
     __device__ void preload_ll(long long n) {
 #pragma unroll
@@ -939,15 +940,39 @@ struct Loop {
         }
     }
 
+    // Wait until the peer's ready word covers push `seq`.  The value last
+    // read is kept in LDS (s_seen): one read that shows a later push covers
+    // every push up to it, so the word is polled only when behind.
+    __device__ bool wait_ready(u64 seq, int iter) const {
+        if (threadIdx.x == 0 && *s_seen < seq) {
+            const u64* p = &a.my_mb->ready[a.peer_slot];
+            const u64 t0 = now_ticks();
+            u64 spins = 0;
+            for (;;) {
+                const u64 v = ld_sys(p);
+                if (v >= seq) { *s_seen = v; break; }
+                if (should_stop(++spins, t0)) { give_up(iter); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        return !aborted();
+    }
+
     // Receive (every workgroup, grid = nwg): wait for the peer's ready word,
     // load this workgroup's chunk of the peer's tx into rx, check it (check
-    // mode), then return the chunk to the peer (credit: its tx chunk may
-    // change again) and count it landed.
-    __device__ bool pull_recv(long long n, u64 seq, int iter) const {
-        if (!poll_ge<true>(&a.my_mb->ready[a.peer_slot], seq, iter)) return false;
+    // mode).  `publish` > 0: then drain, return the chunk to the peer (credit
+    // = seq: its tx chunk may change again, for every push up to seq) and
+    // count `publish` receives of this workgroup landed.  The non-blocking
+    // loop publishes every nb_publish receives (and at the last): the others
+    // are loads and stores only, with no drain between them.
+    __device__ bool pull_recv(long long n, u64 seq, int iter, u64 publish = 1) const {
+        if (!wait_ready(seq, iter)) return false;
         // system-scope acquire (buffer_inv sc0 sc1: the L2's lines of
         // non-local memory, i.e. a peer GPU's tx, are dropped, so every
         // iteration's loads cross the link), completed before any wave loads
+        // (every wave drains; draining only the fencing wave read the same:
+        // profiles/r03_pull_publish_ab.jsonl)
         if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         drain_stores();
         __syncthreads();
@@ -977,12 +1002,13 @@ struct Loop {
                 }
             }
         }
+        if (a.check) check(n, iter);                   // (drains first: sum_chunk)
+        if (!publish) return true;
         drain_stores();                                // loads and stores of every wave
-        if (a.check) check(n, iter);
         __syncthreads();
         if (threadIdx.x == 0) {
             st_sys(&a.peer_mb->credit[a.my_slot][blockIdx.x], seq);
-            __hip_atomic_fetch_add(&a.gbar[kScrLanded], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&a.gbar[kScrLanded], publish, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         return true;
     }
@@ -1184,13 +1210,17 @@ template <int MODE, int GROUP>
 __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
     __shared__ int s_abort;
     __shared__ u64 lds4[4];
-    if (threadIdx.x == 0) s_abort = 0;
-    Loop<MODE> L{a, &s_abort, lds4, nullptr, {}};
+    __shared__ u64 s_seen;
+    if (threadIdx.x == 0) {
+        s_abort = 0;
+        s_seen = 0;
+    }
+    Loop<MODE> L{a, &s_abort, lds4, nullptr, {}, &s_seen};
     const long long n = a.len;
     const u64 nw = (u64)a.nwg;
     if (MODE == MPX_MODE_UNIDIR && GROUP == 0 && blockIdx.x == 0) L.preload_ll(1);   // the ack's byte
     __syncthreads();
-    u64 txs = a.tx_seq0, rxs = a.rx_seq0, done = 0;
+    u64 txs = a.tx_seq0, rxs = a.rx_seq0, done = 0, pending = 0;
     L.post_receives();
     bool ok = true;
     int inflight = 0;
@@ -1217,7 +1247,14 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
                 if (ok) L.send(1, ++txs);
             }
         } else {                                       // mpi_perf.c:95-124
-            ok = L.pull_send(++txs, 0, i) && L.pull_recv(n, ++rxs, i);   // Isend + Irecv, slot `inflight`
+            // Isend + Irecv, slot `inflight`; the receive is published (drain,
+            // credit, landed count) every nb_publish receives and at the last
+            // one — kNbWindow is a multiple of nb_publish, so slot 255 (the
+            // flush) is always a publish point
+            ++pending;
+            const bool pub = (i + 1) % a.nb_publish == 0 || i + 1 == a.iters;
+            ok = L.pull_send(++txs, 0, i) && L.pull_recv(n, ++rxs, i, pub ? pending : 0);
+            if (pub) pending = 0;
             if (ok && inflight == kNbWindow - 1) {
                 // Waitall(255): every workgroup waits until all chunks of
                 // receives 0..i are in (so none runs into the next window

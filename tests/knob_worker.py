@@ -1,8 +1,9 @@
 """GPU worker for tests/test_gpu_engine.py::test_env_knob_variants: runs the
 loopback pair (two ranks on GPU 0) through every mode and both engines with
 every payload checked, under whatever MPX_* knobs its environment sets (libmpx
-reads them once per process, hence a process of its own).  Prints "ok" or
-raises."""
+reads them once per process, hence a process of its own).  "kernel-pull" is
+the kernel engine in pull mode (MPX_XFER_PULL), whose non-blocking receives
+publish on the MPX_NB_PUBLISH schedule too.  Prints "ok" or raises."""
 import os
 import sys
 import threading
@@ -11,8 +12,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import mpx  # noqa: E402
 
 CAP = (1 << 20) + 9
-for engine in ("kernel", "sdma"):
-    with mpx.Context(2, engine) as c:
+for engine in ("kernel", "sdma", "kernel-pull"):
+    pull = engine == "kernel-pull"
+    with mpx.Context(2, "kernel" if pull else engine) as c:
         bufs = []
         for r in range(2):
             tx, rx = c.alloc(0, CAP), c.alloc(0, CAP)
@@ -28,7 +30,7 @@ for engine in ("kernel", "sdma"):
                 def side(r):
                     try:
                         t = c.xfer(mode, 1 - r, r, 1 - r, iters, bufs[r][0], bufs[r][1], n, check_payload=check,
-                                   expect=exp[r][0], expect_ack=exp[r][1], timeout_ms=10000)
+                                   expect=exp[r][0], expect_ack=exp[r][1], timeout_ms=10000, pull=pull)
                         assert t.check_failures == 0
                     except Exception as e:  # noqa: BLE001
                         errs.append(f"{engine} mode {mode} n {n} rank {r}: {e}")
