@@ -466,7 +466,8 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
 PULL_AB_ITERS = 100
 
 
-def push_vs_pull(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, nwg, stream, expect, expect_ack, errs) -> dict:
+def push_vs_pull(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes, nwg, stream, expect, expect_ack,
+                 errs) -> dict:
     """Round 0's pairs at B in both directions of data movement of the
     kernel engine ("try pull as well"): push (the
     headline's form and tuned width) and pull (MPX_XFER_PULL: the receiver's
@@ -494,10 +495,11 @@ def push_vs_pull(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, nwg, stream,
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             out[f"{name}_{label}_GBps"] = rate(mult * nbytes * PULL_AB_ITERS / 1e9, float(t[0]), 2)
     # the pull's own width: unidir at every tuning width (the push's choice
-    # need not be the pull's)
+    # need not be the pull's), within the one-GPU rehearsal's residency cap
     by_width = {}
+    max_wg = one_gpu_push_cap(world) or 256
     for w in sorted({x for x, _ in PUSH_CANDIDATES}):
-        if w * 16 > nbytes:
+        if w * 16 > nbytes or w > max_wg:
             continue
         dist.barrier()
         wall = safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, PULL_AB_ITERS, tx, rx, nbytes, nwg=w, pull=True)
@@ -687,7 +689,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         if engine == "kernel":
             # last: a pull failure (e.g. a peer's tx not mapped) breaks only
             # what comes after it on this context
-            out["push_vs_pull"] = push_vs_pull(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, nwg, stream,
+            out["push_vs_pull"] = push_vs_pull(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes, nwg, stream,
                                                [d[1] for d in descs], [d[2] for d in descs], errs)
         every = [None] * world
         dist.all_gather_object(every, errs[:3])
