@@ -23,6 +23,9 @@
  *
  * Environment (all optional):
  *   MPX_ENGINE=kernel|sdma|rccl   transfer engine (default kernel)
+ *   MPX_XFER_PULL=1               kernel engine: every B-byte payload pulled by
+ *                                 its receiver (libmpx reads it; every rank
+ *                                 of the job inherits it, so both sides agree)
  *   MPX_CHECK=1                   checksum every received payload on the device
  *   MPX_RECV_OUT=<prefix>         write <prefix>.<world_rank>.json at
  *                                 MPI_Finalize: receives completed, bytes and

@@ -120,14 +120,22 @@ GPU_CASES = ["pingpong_p1_b1_i10", "pingpong_p1_b456131_i3", "unidir_p1_b8_i10",
              "unidir_wins_over_nonblocking", "summary_every_1000", "max_int_buffer"]
 
 
+def engine_env(engine: str) -> dict:
+    """the binding's engine (MPX_ENGINE); "kernel-pull": the kernel engine
+    with every B-byte payload pulled by its receiver (MPX_XFER_PULL=1)"""
+    if engine == "kernel-pull":
+        return {"MPX_ENGINE": "kernel", "MPX_XFER_PULL": "1"}
+    return {"MPX_ENGINE": engine}
+
+
 @pytest.mark.gpu
 @needs_bin
-@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "kernel-pull"])
 @pytest.mark.parametrize("case", GPU_CASES)
 def test_patched_reference_receives_match_reference(tmp_path, case, engine):
     c = GOLDEN[case]
     out = str(tmp_path / "recv")
-    p, recs = launch(tmp_path, case, {"MPX_CHECK": "1", "MPX_RECV_OUT": out, "MPX_ENGINE": engine})
+    p, recs = launch(tmp_path, case, {"MPX_CHECK": "1", "MPX_RECV_OUT": out, **engine_env(engine)})
     assert p.returncode == 0, p.stderr[-1500:]
     # pairing printed by the reference's own main (mpi_perf.c:460)
     info = sorted((tuple(int(x) for x in m.groups()) for m in INFO_RE.finditer(p.stderr)))
@@ -174,7 +182,7 @@ def _shim_json(prefix, np_):
 @given(mode=st.sampled_from(["pingpong", "nonblocking", "unidir"]), ppn=st.sampled_from([1, 2]),
        B=st.one_of(st.integers(0, 64), st.sampled_from(LL_EDGES), st.integers(65, 300000),
                    st.integers(300001, 8 << 20)), iters=st.integers(1, 40),
-       window=st.booleans(), engine=st.sampled_from(["kernel", "sdma"]))
+       window=st.booleans(), engine=st.sampled_from(["kernel", "sdma", "kernel-pull"]))
 def test_random_runs_match_the_live_reference(tmp_path, mode, ppn, B, iters, window, engine):
     """A random (loop, ppn, B, iterations) — beyond the golden fixtures — run
     twice: by the compiled reference itself on the host (MPICH shared memory,
@@ -197,7 +205,7 @@ def test_random_runs_match_the_live_reference(tmp_path, mode, ppn, B, iters, win
                       env=dict(os.environ, SHIM_OUT=shim))
     assert ref.returncode == 0, ref.stderr[-800:]
     out = str(d / "recv")
-    env = {"MPX_CHECK": "1", "MPX_RECV_OUT": out, "MPX_ENGINE": engine}
+    env = {"MPX_CHECK": "1", "MPX_RECV_OUT": out, **engine_env(engine)}
     ours = run_bounded(base + sum((["-genv", k, v] for k, v in env.items()), []) + [WRAP, BIN] + args, timeout=60,
                        cwd=d, env=dict(os.environ, **env))
     assert ours.returncode == 0, ours.stderr[-800:]
