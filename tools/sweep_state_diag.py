@@ -39,6 +39,12 @@ def one_mib_arms(c, src, dst):
             print(json.dumps(dict(state=f"after the headline load, round {rnd}", arm=name, sweep=sw)), flush=True)
 
 
+if len(sys.argv) > 2 and sys.argv[2] == "torch":
+    # bench.py's process state: torch initialised on the device first
+    import torch
+    torch.cuda.set_device(0)
+    torch.cuda.synchronize()
+
 with mpx.Context(1) as c:
     src, dst = c.alloc(0, G), c.alloc(0, G)
     if len(sys.argv) > 1 and sys.argv[1] == "onemib":
