@@ -99,7 +99,10 @@ struct Rank {
     bool broken = false;           // a transfer timed out: link state unknown
     int dev = -1;
     char bus_id[32] = {0};
-    unsigned char* tx = nullptr;   // local tx, or the imported rank's tx mapped here (pull mode)
+    unsigned char* tx = nullptr;   // local tx, or the imported rank's tx mapped here (pull mode:
+                                   // on the first pull call, ensure_peer_tx)
+    hipIpcMemHandle_t tx_handle{}; // imported rank: its tx, until mapped
+    bool tx_handle_valid = false;
     unsigned char* rx = nullptr;   // local rx, or the imported rank's rx mapped here
     size_t len = 0;
     Mailbox* mb = nullptr;         // usable from this process
@@ -608,9 +611,29 @@ u64 timeout_ticks(const mpx_xfer_opts* o) {
 // ---------------------------------------------------------------------------
 // engine: kernel
 // ---------------------------------------------------------------------------
+// Pull mode loads from the peer's tx: an imported rank's tx is mapped here on
+// first use (under the context lock: both halves of a pair, or several local
+// ranks, may get here at once), on the device imports are opened on.
+int ensure_peer_tx(mpx_ctx* ctx, Rank& peer, int peer_rank) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (peer.tx) return MPX_OK;
+    if (!peer.imported || !peer.tx_handle_valid)
+        return fail(MPX_ERR_STATE, "pull mode: rank %d's tx is not known here", peer_rank);
+    DeviceGuard g(ctx->import_dev);
+    HIPCK(g.err);
+    void* p = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&p, peer.tx_handle, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(MPX_ERR_HIP, "pull mode: mapping rank %d's tx: %s", peer_rank, hipGetErrorString(e));
+    }
+    ctx->ipc_opened.push_back(p);
+    peer.tx = static_cast<unsigned char*>(p);
+    return MPX_OK;
+}
+
 int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters,
                long long len, const mpx_xfer_opts* o, mpx_timing* t) {
-    (void)ctx;
     XferArgs a{};
     a.tx = me.tx;
     a.rx = me.rx;
@@ -672,7 +695,10 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     // LL messages stay pushes.  A receiving side runs nwg workgroups (one
     // chunk each), unidir group 1 one (it only publishes and takes acks).
     a.pull = (!ll && pull_requested(o)) ? 1 : 0;
-    if (a.pull && !peer.tx) return fail(MPX_ERR_STATE, "rank %d: pull mode needs rank %d's tx mapped", my_rank, peer_rank);
+    if (a.pull && !peer.tx) {
+        TRY(ensure_peer_tx(ctx, peer, peer_rank));
+        a.peer_tx = peer.tx;
+    }
     const int grid = a.pull ? (recvs_len ? a.nwg : 1)
                             : (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;
     // bulk pushes read tx from LDS when one workgroup's chunk fits
@@ -1552,18 +1578,10 @@ int mpx_rank_import(mpx_ctx* ctx, int rank, const void* desc) {
     HIPCK(hipIpcOpenMemHandle(&p, d.rx_handle, hipIpcMemLazyEnablePeerAccess));
     ctx->ipc_opened.push_back(p);
     rk.rx = static_cast<unsigned char*>(p);
-    // tx is mapped for pull mode only: a failure leaves it unmapped (a pull
-    // call then reports MPX_ERR_STATE) and costs the push engines nothing
-    {
-        const hipError_t e = hipIpcOpenMemHandle(&p, d.tx_handle, hipIpcMemLazyEnablePeerAccess);
-        if (e == hipSuccess) {
-            ctx->ipc_opened.push_back(p);
-            rk.tx = static_cast<unsigned char*>(p);
-        } else {
-            DBG("import rank %d: tx not mapped (%s): no pull mode with it\n", rank, hipGetErrorString(e));
-            (void)hipGetLastError();
-        }
-    }
+    // tx is mapped on the first pull-mode call that loads from it
+    // (ensure_peer_tx): a job that never pulls maps nothing more than before
+    rk.tx_handle = d.tx_handle;
+    rk.tx_handle_valid = true;
     rk.ring_bytes = d.ring_bytes;
     if (d.ring_bytes) {
         HIPCK(hipIpcOpenMemHandle(&p, d.ring_handle, hipIpcMemLazyEnablePeerAccess));
