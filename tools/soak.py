@@ -5,9 +5,13 @@ same plan from one seed; after every call each rank compares its rx with the
 peer's tx (the bytes the reference's last receive leaves in rx), and in check
 mode every payload is checksummed on the device.
 
-    python tools/soak.py threads <calls> <seed>          two ranks, one process
-    python tools/soak.py procs <calls> <seed>            two processes over IPC
-    python tools/soak.py worker <dir> <rank> <calls> <seed>   (one process of `procs`)
+    python tools/soak.py threads <calls> <seed> [engine]   two ranks, one process
+    python tools/soak.py procs <calls> <seed> [engine]     two processes over IPC
+    python tools/soak.py worker <dir> <rank> <calls> <seed> <engine>   (one process of `procs`)
+
+engine: kernel (default; push and pull calls) or sdma (push only).  With a
+negative-control knob set (MPX_TEST_NO_POSTED=1, MPX_TEST_NO_PULL_WAIT=1) the
+soak must report failures: that is what shows it can see the races.
 
 Prints one JSON line per form: calls run, failures (with the first few),
 seconds.  Exit status 1 on any failure.
@@ -30,7 +34,7 @@ EDGES = [0, 1, 15, 16, 17, 2047, 2048, 2049, 4096, 8191, 8192, 8193, 65536, 6553
 MODES = [mpx.MODE_PINGPONG, mpx.MODE_NONBLOCKING, mpx.MODE_UNIDIR]
 
 
-def plan(calls, seed):
+def plan(calls, seed, engine="kernel"):
     rng = random.Random(seed)
     out = []
     for k in range(calls):
@@ -40,7 +44,8 @@ def plan(calls, seed):
             iters = rng.choice([1, 2, 17, 255, 256, 257, 300]) if n <= (1 << 20) else rng.randint(1, 20)
         else:
             iters = rng.randint(1, 40) if n <= (1 << 20) else rng.randint(1, 8)
-        out.append(dict(mode=mode, n=n, iters=iters, check=rng.random() < 0.6, pull=rng.random() < 0.5,
+        pull = rng.random() < 0.5 and engine == "kernel"
+        out.append(dict(mode=mode, n=n, iters=iters, check=rng.random() < 0.6, pull=pull,
                         nwg=rng.choice([0, 0, 1, 3, 8, 64, 128, 256]), stream=rng.random() < 0.3,
                         refill=rng.random() < 0.2, key=rng.getrandbits(32)))
     return out
@@ -98,10 +103,10 @@ class Sums:
         return d[n]
 
 
-def threads(calls, seed):
-    steps = plan(calls, seed)
+def threads(calls, seed, engine="kernel"):
+    steps = plan(calls, seed, engine)
     t0 = time.time()
-    with mpx.Context(2, "kernel") as c:
+    with mpx.Context(2, engine) as c:
         bufs = []
         for r in range(2):
             tx, rx = c.alloc(0, CAP), c.alloc(0, CAP)
@@ -127,14 +132,14 @@ def threads(calls, seed):
         for t in th:
             t.join()
     fails = out[0] + out[1]
-    return dict(form="threads", calls=calls, seed=seed, failures=len(fails), first=fails[:4],
+    return dict(form="threads", engine=engine, calls=calls, seed=seed, failures=len(fails), first=fails[:4],
                 seconds=round(time.time() - t0, 1))
 
 
-def worker(d, rank, calls, seed):
-    steps = plan(calls, seed)
+def worker(d, rank, calls, seed, engine):
+    steps = plan(calls, seed, engine)
     peer = 1 - rank
-    c = mpx.Context(2, "kernel")
+    c = mpx.Context(2, engine)
     tx, rx = c.alloc(0, CAP), c.alloc(0, CAP)
     c.fill(tx, CAP, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, rank, peer, 0))
     c.attach(rank, 0, tx, rx, CAP)
@@ -158,11 +163,12 @@ def worker(d, rank, calls, seed):
     c.close()
 
 
-def procs(calls, seed):
+def procs(calls, seed, engine="kernel"):
     import tempfile
     d = tempfile.mkdtemp(prefix="soak_")
     t0 = time.time()
-    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "worker", d, str(r), str(calls), str(seed)])
+    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "worker", d, str(r), str(calls), str(seed),
+                            engine])
           for r in (0, 1)]
     rcs = []
     for p in ps:
@@ -175,14 +181,15 @@ def procs(calls, seed):
     for r in (0, 1):
         path = os.path.join(d, f"result_{r}.json")
         fails += json.load(open(path)) if os.path.exists(path) else [dict(rank=r, what=f"no result (rc {rcs[r]})")]
-    return dict(form="procs", calls=calls, seed=seed, failures=len(fails), first=fails[:4], rcs=rcs,
+    return dict(form="procs", engine=engine, calls=calls, seed=seed, failures=len(fails), first=fails[:4], rcs=rcs,
                 seconds=round(time.time() - t0, 1))
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "worker":
-        worker(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))
+        worker(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), sys.argv[6])
         sys.exit(0)
-    res = (threads if sys.argv[1] == "threads" else procs)(int(sys.argv[2]), int(sys.argv[3]))
+    res = (threads if sys.argv[1] == "threads" else procs)(int(sys.argv[2]), int(sys.argv[3]),
+                                                            sys.argv[4] if len(sys.argv) > 4 else "kernel")
     print(json.dumps(res), flush=True)
     sys.exit(1 if res["failures"] else 0)
