@@ -110,7 +110,8 @@ typedef struct mpx_timing {
                                  launch (k_copy_steps), 6 = the same with the
                                  next copy's loads in flight (k_copy_pipe),
                                  7 = bulk payloads pulled by the receiver
-                                 (MPX_XFER_PULL)                                */
+                                 (MPX_XFER_PULL), 8 = the SDMA engine's
+                                 pulled form                                    */
     int32_t check_failures;   /* iterations whose payload checksum mismatched  */
     uint64_t check_iters;     /* iterations whose payload was checksummed      */
     /* receive accounting, as the reference's loop completes receives: every
@@ -140,14 +141,16 @@ typedef struct mpx_xfer_opts {
    hint on top of their system-scope write-through policy (sc0 sc1 nt instead
    of sc0 sc1).  Visibility is unchanged, so the two sides need not agree. */
 #define MPX_XFER_STREAM 1
-/* mpx_xfer_opts.flags: kernel engine only — every B-byte payload is PULLED:
-   the sender publishes "tx holds message k" (one store into the receiver's
-   mailbox) and the receiver's kernel loads the bytes from the sender's
-   peer-mapped tx into its own rx, instead of the sender storing them into
-   the receiver's rx.  LL messages (<= the link's LL threshold) and the unidir
-   1-byte ack stay pushes.  Both sides of a link must set it alike (as nwg);
-   the SDMA and RCCL engines refuse it (MPX_ERR_UNSUPPORTED).  The environment
-   variable MPX_XFER_PULL=1 makes it the kernel engine's default. */
+/* mpx_xfer_opts.flags: every B-byte payload is PULLED: the sender publishes
+   "tx holds message k" (one store into the receiver's mailbox) and the
+   receiver loads the bytes from the sender's peer-mapped tx into its own rx —
+   the kernel engine with its receiving kernel's loads, the SDMA engine with a
+   copy on the receiver's stream — instead of the sender storing them into the
+   receiver's rx.  Kernel engine: LL messages (<= the link's LL threshold)
+   stay pushes; both engines push the unidir 1-byte ack.  Both sides of a
+   link must set it alike (as nwg); the RCCL engine refuses it
+   (MPX_ERR_UNSUPPORTED).  The environment variable MPX_XFER_PULL=1 makes it
+   the kernel and SDMA engines' default. */
 #define MPX_XFER_PULL 2
 
 /* opaque context */

@@ -21,7 +21,7 @@ constexpr int kStageMaxBytes = 60 << 10; // LDS-staged tx chunk per workgroup, m
 
 // Protocol ids reported in mpx_timing.protocol
 enum Proto { kProtoLL = 0, kProtoBulk = 1, kProtoSdma = 2, kProtoRccl = 3, kProtoCopy = 4, kProtoCopySteps = 5,
-             kProtoCopyPipe = 6, kProtoPull = 7 };
+             kProtoCopyPipe = 6, kProtoPull = 7, kProtoSdmaPull = 8 };
 
 // One rank's receive mailbox, in that rank's HBM (uncached / fine-grained so a
 // poll sees stores that arrive over xGMI).  Written ONLY by the peers, polled

@@ -810,6 +810,7 @@ struct SdmaOps {
     const u64* rxb = nullptr;
     int launches = 0;
     int skip = 0;               // test knob: 1 + iteration whose copy is skipped
+    bool pull = false;          // MPX_XFER_PULL: B-byte payloads copied by the receiver's stream
     // The flag store is a one-lane kernel ordered after the copy on this
     // stream (hipStreamWriteValue64 measured slower, 10.9 vs 8.6 us per
     // iteration, profiles/r01_sdma_signal_ab.jsonl).  Waits are bounded
@@ -831,11 +832,84 @@ struct SdmaOps {
         ++launches;
         return MPX_OK;
     }
+    // Pull mode (the kernel engine's k_xfer_pull in stream form).  A send
+    // publishes "tx holds push seq" in the peer's ready word (tx is read-only
+    // while the loop runs, and the reference re-sends the same buffer).
+    int pull_send(u64 seq) {
+        HIPCK(launch_signal(&peer.mb->ready[my_slot], txb, seq, me.stream));
+        ++launches;
+        return MPX_OK;
+    }
+    // A receive waits for the peer's ready word, copies the peer's tx into rx
+    // on this rank's stream (a copy engine reading the peer's HBM across
+    // GPUs), then, when `publish`, hands the peer's tx back (credit = seq,
+    // for every push up to seq).
+    int pull_recv(long long n, u64 seq, bool publish, bool skip_copy) {
+        HIPCK(launch_wait(&me.mb->ready[peer_slot], rxb, seq, me.status, tmo, me.stream));
+        ++launches;
+        if (n > 0 && !skip_copy) {
+            HIPCK(hipMemcpyAsync(me.rx, peer.tx, (size_t)n, sdma_kind(&me != &peer && same_device(me, peer)),
+                                 me.stream));
+            ++launches;
+        }
+        if (!publish) return MPX_OK;
+        HIPCK(launch_signal(&peer.mb->credit[my_slot][0], rxb, seq, me.stream));
+        ++launches;
+        return MPX_OK;
+    }
+    // every one of this side's sends up to `seq` copied by the peer
+    int wait_pulled(u64 seq) {
+        HIPCK(launch_wait(&me.mb->credit[peer_slot][0], txb, seq, me.status, tmo, me.stream));
+        ++launches;
+        return MPX_OK;
+    }
+    // one iteration of the pulled loop (see step)
+    int pull_step(int mode, int group, long long len, int i, int iters, u64 tx0, u64 rx0, bool check, int* inflight) {
+        const bool sk = skip == i + 1;
+        if (mode == MPX_MODE_PINGPONG) {
+            if (group == 1) {
+                TRY(pull_send(tx0 + i + 1));
+                TRY(pull_recv(len, rx0 + i + 1, true, sk));
+                if (check) TRY(stream_check(me, len, i, iters));
+            } else {
+                TRY(pull_recv(len, rx0 + i + 1, true, sk));
+                if (check) TRY(stream_check(me, len, i, iters));
+                TRY(pull_send(tx0 + i + 1));
+            }
+        } else if (mode == MPX_MODE_UNIDIR) {
+            if (group == 1) {
+                TRY(pull_send(tx0 + i + 1));
+                TRY(wait(rx0 + i + 1));                      // the 1-byte ack, pushed
+                if (check) TRY(stream_check(me, 1, i, iters));
+            } else {
+                TRY(pull_recv(len, rx0 + i + 1, true, sk));
+                if (check) TRY(stream_check(me, len, i, iters));
+                TRY(push(1, tx0 + i + 1, true, false));      // Send(tx, 1): always one byte, pushed
+            }
+        } else {
+            // Isend + Irecv; the receive is complete on this stream once its
+            // copy ran; credits go back on the push's publish schedule
+            TRY(pull_send(tx0 + i + 1));
+            TRY(pull_recv(len, rx0 + i + 1, nb_publishes(i, iters), sk));
+            if (check) TRY(stream_check(me, len, i, iters));
+            if (*inflight == kNbWindow - 1) {
+                // Waitall(255): the peer's copies of sends 0..254; the
+                // receives of slots 0..254 are done (stream order) — count them
+                TRY(wait_pulled(tx0 + i));
+                if (check) HIPCK(launch_account(me.status, me.csum, i - *inflight, *inflight, len, me.stream));
+                *inflight = 0;
+            } else {
+                ++*inflight;
+            }
+        }
+        return MPX_OK;
+    }
     // one iteration i of the loop (mpi_perf.c:70-82, 95-124, 132-144), seqs
     // relative to tx0 / rx0; check mode checksums + poisons each received
     // payload where the reference's Recv returns (before the reply / ack);
     // *inflight is the non-blocking window fill
     int step(int mode, int group, long long len, int i, int iters, u64 tx0, u64 rx0, bool check, int* inflight) {
+        if (pull) return pull_step(mode, group, len, i, iters, tx0, rx0, check, inflight);
         const bool sk = skip == i + 1;
         if (mode == MPX_MODE_PINGPONG) {
             if (group == 1) {
@@ -937,14 +1011,15 @@ bool sdma_graphs_enabled() {
 }
 
 int sdma_chunk_graph(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, long long len,
-                     u64 tmo, int count, hipGraphExec_t* out) {
-    const SdmaKey key{mode, group, peer_rank, len, tmo, count};
+                     u64 tmo, int count, hipGraphExec_t* out, bool pull = false) {
+    const SdmaKey key{mode + (pull ? 8 : 0), group, peer_rank, len, tmo, count};
     auto it = me.sdma_graphs.find(key);
     if (it != me.sdma_graphs.end()) {
         *out = it->second;
         return MPX_OK;
     }
     SdmaOps cap{me, peer, my_rank, peer_rank, tmo, me.scratch + kScrSeqBase, me.scratch + kScrSeqBase + 1};
+    cap.pull = pull;
     HIPCK(hipStreamBeginCapture(me.stream, hipStreamCaptureModeThreadLocal));
     int inflight = 0, st = MPX_OK;
     for (int j = 0; j < count && st == MPX_OK; ++j) st = cap.step(mode, group, len, j, count, 0, 0, false, &inflight);
@@ -968,12 +1043,13 @@ int sdma_chunk_graph(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode,
 
 
 int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters, long long len,
-             const mpx_xfer_opts* o, mpx_timing* t) {
+             const mpx_xfer_opts* o, mpx_timing* t, bool pull) {
     SdmaOps op{me, peer, my_rank, peer_rank, timeout_ticks(o)};
     op.skip = skip_push_knob();
+    op.pull = pull;
     const int check = (o && o->check) ? 1 : 0;
     const int slots = link_slots(me, peer, len);
-    if (check && mode == MPX_MODE_NONBLOCKING && len > 0 && slots > 1 && (!me.ring || !peer.ring))
+    if (!pull && check && mode == MPX_MODE_NONBLOCKING && len > 0 && slots > 1 && (!me.ring || !peer.ring))
         return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
     if (check) HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
     me.status->err = 0;
@@ -987,8 +1063,9 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     const int chunks = graphs ? iters / kSdmaChunk : 0;
     const int rest = graphs && iters % kSdmaChunk >= kSdmaGraphMin ? iters % kSdmaChunk : 0;
     hipGraphExec_t full = nullptr, tail = nullptr;
-    if (chunks > 0) TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, kSdmaChunk, &full));
-    if (rest > 0) TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, rest, &tail));
+    if (chunks > 0)
+        TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, kSdmaChunk, &full, pull));
+    if (rest > 0) TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, group, len, op.tmo, rest, &tail, pull));
     if (full || tail) HIPCK(launch_seqbase(me.scratch + kScrSeqBase, txs0, rxs0, 0, me.stream));
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
@@ -1000,7 +1077,7 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
         TRY(op.signal_abs(&peer.mb->posted[my_rank], call));
         if (mode == MPX_MODE_NONBLOCKING || group == 1) TRY(op.wait_abs(&me.mb->posted[peer_rank], call));
     }
-    if (check && mode == MPX_MODE_NONBLOCKING) {
+    if (check && mode == MPX_MODE_NONBLOCKING && !pull) {
         TRY(op.nb_checked(iters, len, txs0, rxs0, slots));
     } else {
         for (int c = 0; c < chunks; ++c) HIPCK(hipGraphLaunch(full, me.stream));
@@ -1008,10 +1085,19 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
         int inflight = 0;
         const int replayed = chunks * kSdmaChunk + rest;
         for (int i = replayed; i < iters; ++i) TRY(op.step(mode, group, len, i, iters, txs0, rxs0, check, &inflight));
-        if (mode == MPX_MODE_NONBLOCKING && iters > 0 && (iters % kNbWindow) != 0) TRY(op.wait(rxs0 + iters));
+        if (pull) {
+            // pulled: every receive is complete on this stream; the final
+            // Waitall's receives are counted (check mode), and a side that
+            // sent B-byte payloads waits for the peer's copies of its tx
+            if (mode == MPX_MODE_NONBLOCKING && check && inflight > 0)
+                HIPCK(launch_account(me.status, me.csum, iters - inflight, inflight, len, me.stream));
+            if (iters > 0 && (mode != MPX_MODE_UNIDIR || group == 1)) TRY(op.wait_pulled(txs0 + iters));
+        } else if (mode == MPX_MODE_NONBLOCKING && iters > 0 && (iters % kNbWindow) != 0) {
+            TRY(op.wait(rxs0 + iters));
+        }
         // every receive of ping-pong / unidir is complete here; the device
         // counts them and digests their checksums
-        if (check && iters > 0)
+        if (check && iters > 0 && mode != MPX_MODE_NONBLOCKING)
             HIPCK(launch_account(me.status, me.csum, 0, iters,
                                  (mode == MPX_MODE_UNIDIR && group == 1) ? 1 : len, me.stream));
     }
@@ -1023,7 +1109,7 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     t->device_s = ms * 1e-3;
     t->launches = op.launches + (chunks + (tail ? 1 : 0));   // graph replays count once each
     t->nwg = 0;
-    t->protocol = kProtoSdma;
+    t->protocol = pull ? kProtoSdmaPull : kProtoSdma;
     // check mode: counted on the device (k_account); otherwise the loop's
     // structure fixes the count
     t->recv_done = check ? __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE)
@@ -1620,9 +1706,9 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
     if ((size_t)buff_len > me.len || (!rccl && (size_t)buff_len > peer.len))
         return fail(MPX_ERR_INVALID, "buff_len %d exceeds an attached length (%zu, %zu)", buff_len, me.len, peer.len);
     const int check = opts && opts->check;
-    if (opts && (opts->flags & MPX_XFER_PULL) && ctx->engine != MPX_ENGINE_KERNEL)
-        return fail(MPX_ERR_UNSUPPORTED, "pull mode (MPX_XFER_PULL) is a kernel-engine mode");
-    const bool pull = ctx->engine == MPX_ENGINE_KERNEL && pull_requested(opts);
+    if (opts && (opts->flags & MPX_XFER_PULL) && ctx->engine == MPX_ENGINE_RCCL)
+        return fail(MPX_ERR_UNSUPPORTED, "pull mode (MPX_XFER_PULL): the kernel and SDMA engines only");
+    const bool pull = ctx->engine != MPX_ENGINE_RCCL && pull_requested(opts);
     if (check) TRY(ensure_csum(me, iters));
     // (pull mode receives into rx in order: no receive ring)
     if (check && !pull && mode == MPX_MODE_NONBLOCKING && ctx->engine != MPX_ENGINE_RCCL) {
@@ -1639,7 +1725,10 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
         case MPX_ENGINE_KERNEL:
             st = run_kernel(ctx, me, peer, my_rank, peer_rank, mode, my_group, iters, buff_len, opts, t);
             break;
-        case MPX_ENGINE_SDMA: st = run_sdma(me, peer, my_rank, peer_rank, mode, my_group, iters, buff_len, opts, t); break;
+        case MPX_ENGINE_SDMA:
+            st = pull && buff_len > 0 && !peer.tx ? ensure_peer_tx(ctx, peer, peer_rank) : MPX_OK;
+            if (st == MPX_OK) st = run_sdma(me, peer, my_rank, peer_rank, mode, my_group, iters, buff_len, opts, t, pull);
+            break;
         default: st = run_rccl(me, peer, my_rank, peer_rank, mode, my_group, iters, buff_len, opts, t); break;
     }
     if (st != MPX_OK) return st;
@@ -1705,14 +1794,17 @@ int mpx_xfer_prepare(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer
     if (ctx->engine != MPX_ENGINE_SDMA || (opts && opts->check) || !sdma_graphs_enabled() || iters < kSdmaGraphMin)
         return MPX_OK;
     if (!peer.local && !peer.imported) return fail(MPX_ERR_STATE, "peer rank %d is unknown", peer_rank);
+    const bool pull = pull_requested(opts);   // pulled chunks copy from the peer's tx: mapped first
+    if (pull && buff_len > 0 && !peer.tx) TRY(ensure_peer_tx(ctx, peer, peer_rank));
     DeviceGuard g(me.dev);
     HIPCK(g.err);
     const u64 tmo = timeout_ticks(opts);
     hipGraphExec_t x = nullptr;
     if (iters / kSdmaChunk > 0)
-        TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, my_group, buff_len, tmo, kSdmaChunk, &x));
+        TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, my_group, buff_len, tmo, kSdmaChunk, &x, pull));
     if (iters % kSdmaChunk >= kSdmaGraphMin)
-        TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, my_group, buff_len, tmo, iters % kSdmaChunk, &x));
+        TRY(sdma_chunk_graph(me, peer, my_rank, peer_rank, mode, my_group, buff_len, tmo, iters % kSdmaChunk, &x,
+                             pull));
     return MPX_OK;
 }
 

@@ -287,11 +287,12 @@ static void *rank_main(void *arg)
                 if (files.log_fp) fputs(line, files.log_fp);
                 if (files.gpu_fp) {
                     const double gbps = my_time > 0 ? (double)tm.bytes / my_time / 1e9 : 0.0;
-                    static const char *proto[] = {"ll", "bulk", "sdma", "rccl", "copy", "copy_steps", "copy_pipe", "pull"};
+                    static const char *proto[] = {"ll", "bulk", "sdma", "rccl", "copy", "copy_steps", "copy_pipe", "pull",
+                                                 "sdma_pull"};
                     fprintf(files.gpu_fp, "%s,%s,%d,%s,%d,%d,%d,%d,%d,%d,%.4f,%.4f,%.3f,%s,%d,%llu,%d,%lld,%llu,%llu\n", ts,
                             opt.uuid, r, mpxh_engine_name(opt.engine), xfer_mode(), dev_of[r], peer, dev_of[peer], B,
                             opt.iters, my_time * 1e3, tm.device_s * 1e3, gbps,
-                            (tm.protocol >= 0 && tm.protocol <= 7) ? proto[tm.protocol] : "?", tm.nwg,
+                            (tm.protocol >= 0 && tm.protocol <= 8) ? proto[tm.protocol] : "?", tm.nwg,
                             (unsigned long long)tm.check_iters, tm.check_failures, run_idx,
                             (unsigned long long)tm.recv_done, (unsigned long long)tm.recv_digest);
                 }

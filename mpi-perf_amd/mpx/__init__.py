@@ -35,7 +35,7 @@ PATTERN_SEED = 0x6D70695F70657266
 MAX_RANKS = 64
 RANK_DESC_BYTES = 512
 RCCL_ID_BYTES = 128
-PROTOCOLS = {0: "ll", 1: "bulk", 2: "sdma", 3: "rccl", 4: "copy", 5: "copy_steps", 6: "copy_pipe", 7: "pull"}
+PROTOCOLS = {0: "ll", 1: "bulk", 2: "sdma", 3: "rccl", 4: "copy", 5: "copy_steps", 6: "copy_pipe", 7: "pull", 8: "sdma_pull"}
 
 
 class Timing(C.Structure):

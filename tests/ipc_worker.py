@@ -21,8 +21,8 @@ SIZES = (1, 8, 4097, 8191, 8192, 8193, 65541, 1 << 20)
 def main():
     d, rank = sys.argv[1], int(sys.argv[2])
     engine = sys.argv[3] if len(sys.argv) > 3 else "kernel"
-    pull = engine == "kernel-pull"   # the kernel engine in pull mode (MPX_XFER_PULL)
-    engine = "kernel" if pull else engine
+    pull = engine.endswith("-pull")   # kernel-pull / sdma-pull: that engine in pull mode (MPX_XFER_PULL)
+    engine = engine[:-len("-pull")] if pull else engine
     # "cross": rank r on GPU r (the pair moves its bytes over xGMI); else GPU 0
     dev = rank if len(sys.argv) > 4 and sys.argv[4] == "cross" and not os.environ.get("MPX_MULTI_REHEARSE") else 0
     peer = 1 - rank

@@ -3,7 +3,7 @@ loopback pair (two ranks on GPU 0) through every mode and both engines with
 every payload checked, under whatever MPX_* knobs its environment sets (libmpx
 reads them once per process, hence a process of its own).  "kernel-pull" is
 the kernel engine in pull mode (MPX_XFER_PULL), whose non-blocking receives
-publish on the MPX_NB_PUBLISH schedule too.  Prints "ok" or raises."""
+publish on the MPX_NB_PUBLISH schedule too; "sdma-pull" the SDMA engine's.  Prints "ok" or raises."""
 import os
 import sys
 import threading
@@ -12,9 +12,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import mpx  # noqa: E402
 
 CAP = (1 << 20) + 9
-for engine in ("kernel", "sdma", "kernel-pull"):
-    pull = engine == "kernel-pull"
-    with mpx.Context(2, "kernel" if pull else engine) as c:
+for engine in ("kernel", "sdma", "kernel-pull", "sdma-pull"):
+    pull = engine.endswith("-pull")
+    with mpx.Context(2, engine[:-len("-pull")] if pull else engine) as c:
         bufs = []
         for r in range(2):
             tx, rx = c.alloc(0, CAP), c.alloc(0, CAP)

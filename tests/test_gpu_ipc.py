@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("engine", ["kernel", "sdma", "kernel-pull"])
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "kernel-pull", "sdma-pull"])
 def test_two_process_ipc_pair(tmp_path, engine):
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "ipc_worker.py"), str(tmp_path), str(r), engine],
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in (0, 1)]
@@ -37,3 +37,5 @@ def test_two_process_ipc_pair(tmp_path, engine):
             if engine == "kernel-pull":   # B-byte payloads pulled (protocol 7) above the 2 KiB LL threshold
                 ll = x["mode"] != 1 and x["n"] <= 2048
                 assert x["protocol"] == (0 if ll else 7), (r, x)
+            if engine == "sdma-pull":     # every size pulled by the receiver's stream
+                assert x["protocol"] == 8, (r, x)

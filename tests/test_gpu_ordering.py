@@ -144,10 +144,11 @@ def test_pull_lagging_receiver_fails_without_the_wait(monkeypatch):
 
 @pytest.mark.parametrize("check", [False, True])
 @pytest.mark.parametrize("mode", list(MODES))
-def test_pull_rx_read_between_calls_threads(mode, check):
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+def test_pull_rx_read_between_calls_threads(engine, mode, check):
     n, iters = RACE_CASES[0]
     it = 300 if mode == "nonblocking" else iters
-    out = run_threads(lambda c, r, tx, rx, s: O.race(c, r, tx, rx, s, MODES[mode], check, n, it, pull=True))
+    out = run_threads(lambda c, r, tx, rx, s: O.race(c, r, tx, rx, s, MODES[mode], check, n, it, pull=True), engine)
     assert_race_ok(out)
 
 

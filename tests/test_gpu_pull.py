@@ -1,8 +1,9 @@
-"""Pull mode (MPX_XFER_PULL) of the kernel engine: parity on the GPU.
+"""Pull mode (MPX_XFER_PULL) of the kernel and SDMA engines: parity on the GPU.
 
 The reference's three loops (/root/reference/mpi_perf.c:66-145) with every
 B-byte payload loaded by its RECEIVER from the sender's peer-mapped tx
-(k_xfer_pull) instead of stored by the sender into the receiver's rx — the
+(k_xfer_pull; the SDMA engine: a copy on the receiver's stream) instead of
+stored by the sender into the receiver's rx — the
 "try pull as well" of SURVEY.md §7 step 4.  What a caller sees must not
 change: the same bytes land (every payload checksummed against the oracle's
 pattern checksum or the peer's tx), the same receives are counted and
@@ -22,21 +23,29 @@ pytestmark = pytest.mark.gpu
 
 MODES = [mpx.MODE_PINGPONG, mpx.MODE_NONBLOCKING, mpx.MODE_UNIDIR]
 PAIR_SIZES = [0, 1, 8, 2048, 2049, 4097, 8193, 65541, 456131, 4 << 20]
-PROTO_LL, PROTO_PULL = 0, 7
+PROTO_LL, PROTO_PULL, PROTO_SDMA_PULL = 0, 7, 8
 LL_MAX_ONE_GPU = 2048      # ll_max_bytes(same_device): LL messages stay pushes
 GOLDEN = {c["name"]: c for c in O.golden()["cases"]}
 
 
-def _pulled(mode, n):
-    return mode == mpx.MODE_NONBLOCKING or n > LL_MAX_ONE_GPU
+def _proto(engine, mode, n):
+    """the protocol a pulled call reports: the SDMA engine pulls every size,
+    the kernel engine's LL messages stay pushes"""
+    if engine == "sdma":
+        return PROTO_SDMA_PULL
+    return PROTO_PULL if (mode == mpx.MODE_NONBLOCKING or n > LL_MAX_ONE_GPU) else PROTO_LL
 
 
+ENGINES = ["kernel", "sdma"]
+
+
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("mode", MODES)
-def test_pull_pair_every_payload(mode):
+def test_pull_pair_every_payload(mode, engine):
     """Every size class (0 B, LL sizes that stay pushes, ragged bulk sizes,
     4 MiB), every payload checksummed, the reference's receive count, the
     algorithmic bytes, the protocol, and the final rx = the peer's tx."""
-    P = Pairs("kernel", 1, 4 << 20)
+    P = Pairs(engine, 1, 4 << 20)
     try:
         for n in PAIR_SIZES:
             iters = 300 if (mode == mpx.MODE_NONBLOCKING and n <= 65541) else 7
@@ -47,7 +56,7 @@ def test_pull_pair_every_payload(mode):
                 assert t.check_iters == iters and t.check_failures == 0, (n, r)
                 assert t.recv_done == (O.lib().oracle_nb_waited(iters) if mode == mpx.MODE_NONBLOCKING else iters)
                 assert t.bytes == n * iters * (1 if mode == mpx.MODE_UNIDIR else 2)
-                assert t.protocol == (PROTO_PULL if _pulled(mode, n) else PROTO_LL), (n, r, t.protocol)
+                assert t.protocol == _proto(engine, mode, n), (n, r, t.protocol)
             for r in (0, 1):
                 m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else n
                 assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (n, r)
@@ -90,8 +99,9 @@ def _digest_cases():
     return out
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("name", _digest_cases())
-def test_pull_receive_digest_matches_reference(name):
+def test_pull_receive_digest_matches_reference(name, engine):
     """The golden case's pairs, mode, B, iters and runs in pull mode: each
     rank's device-counted receives, bytes and digest equal the compiled
     reference's ranks' (PMPI shim)."""
@@ -102,7 +112,7 @@ def test_pull_receive_digest_matches_reference(name):
     iters = int(a[a.index("-i") + 1]) if "-i" in a else 10
     B = int(a[a.index("-b") + 1]) if "-b" in a else 456131
     mode = mpx.MODE_UNIDIR if "-u" in a else (mpx.MODE_NONBLOCKING if "-x" in a else mpx.MODE_PINGPONG)
-    P = Pairs("kernel", ppn, B)
+    P = Pairs(engine, ppn, B)
     try:
         digest = {r: [0, 0, 0] for r in range(2 * ppn)}
         for _ in range(runs):
@@ -124,12 +134,13 @@ def test_pull_receive_digest_matches_reference(name):
 NB_ITERS = [1, 254, 255, 256, 257, 511, 512, 600]
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("n", [0, 1, 4097, 65541, 456131])
-def test_pull_nonblocking_every_payload_seeded(n):
+def test_pull_nonblocking_every_payload_seeded(n, engine):
     """-x 1 pulled, every window shape: every receive checksummed on the
     device; the Waitall receives (iters - iters // 256, mpi_perf.c:108-111)
     counted and digested; rx ends holding the last payload."""
-    P = Pairs("kernel", 1, max(n, 1), fill="seeded")
+    P = Pairs(engine, 1, max(n, 1), fill="seeded")
     try:
         for iters in NB_ITERS:
             out, errs = P.run(mpx.MODE_NONBLOCKING, n, iters, pull=True)
@@ -148,14 +159,15 @@ def test_pull_nonblocking_every_payload_seeded(n):
         P.close()
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("skip", [1, 7, 256])
-def test_pull_lost_payload_fails_the_check(monkeypatch, mode, skip):
+def test_pull_lost_payload_fails_the_check(monkeypatch, mode, skip, engine):
     """MPX_TEST_SKIP_PUSH=k in pull mode: the k-th receive of each call loads
     nothing (its ready word and credit still go), so check mode must report
     the receive whose bytes never came."""
     monkeypatch.setenv("MPX_TEST_SKIP_PUSH", str(skip))
-    P = Pairs("kernel", 1, 65541, fill="seeded")
+    P = Pairs(engine, 1, 65541, fill="seeded")
     try:
         out, errs = P.run(mode, 65541, 300, pull=True)
         for r in (0, 1):
@@ -165,11 +177,13 @@ def test_pull_lost_payload_fails_the_check(monkeypatch, mode, skip):
         P.close()
 
 
-def test_push_and_pull_calls_share_a_link():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_push_and_pull_calls_share_a_link(engine):
     """One link alternating push and pull calls, across protocols, sizes and
     widths: the sequence numbers, credits and the receive-posted word stay
-    consistent, every payload checked."""
-    P = Pairs("kernel", 1, 1 << 20, fill="pattern")
+    consistent, every payload checked.  (Unchecked calls too: the SDMA
+    engine replays graph-captured chunks of 256 iterations there.)"""
+    P = Pairs(engine, 1, 1 << 20, fill="pattern")
     try:
         plan = [(0, 100000, 3, 0), (1, 1000, 600, 0), (2, 300000, 4, 5), (0, 8, 5, 0), (1, 1 << 20, 3, 64),
                 (2, 4096, 9, 0), (0, 65541, 7, 3), (1, 0, 300, 0), (2, 1, 5, 0), (1, 4097, 257, 2)]
@@ -178,6 +192,11 @@ def test_push_and_pull_calls_share_a_link():
                 out, errs = P.run(mode, n, it, nwg=nwg, pull=pull)
                 assert not errs, (mode, n, pull, errs)
                 assert all(out[r].check_failures == 0 and out[r].check_iters == it for r in (0, 1))
+                out, errs = P.run(mode, n, it, nwg=nwg, pull=pull, check=False)
+                assert not errs, (mode, n, pull, "unchecked", errs)
+                for r in (0, 1):
+                    m = 1 if (mode == mpx.MODE_UNIDIR and r == 0) else n
+                    assert P.c.checksum(P.bufs[r][1], m) == P.c.checksum(P.bufs[P.peer(r)][0], m), (mode, n, pull, r)
     finally:
         P.close()
 
@@ -212,12 +231,13 @@ def test_pull_max_size_pairs_every_mode():
         P.close()
 
 
-def test_pull_self_pair_nonblocking():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_pull_self_pair_nonblocking(engine):
     """A rank paired with itself (Isend + Irecv to itself) in pull mode: it
     loads its own tx; the oracle's pattern checksum and Waitall count."""
     cap = 456131
     key = mpx.pattern_key(mpx.PATTERN_SEED, 0, 0, 7)
-    c = mpx.Context(1, "kernel")
+    c = mpx.Context(1, engine)
     try:
         tx, rx = c.alloc(0, cap), c.alloc(0, cap)
         c.fill(tx, cap, mpx.FILL_SPLITMIX, key)
@@ -229,33 +249,39 @@ def test_pull_self_pair_nonblocking():
                 t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, n, check_payload=True, expect=want,
                            timeout_ms=10000, pull=True)
                 k = O.lib().oracle_nb_waited(iters)
-                assert t.protocol == PROTO_PULL and t.check_iters == iters and t.check_failures == 0
+                assert t.protocol == _proto(engine, 1, n) and t.check_iters == iters and t.check_failures == 0
                 assert t.recv_done == k and t.recv_digest == (k * want) & 0xFFFFFFFFFFFFFFFF, (n, iters)
                 assert c.checksum(rx, n) == want
     finally:
         c.close()
 
 
-def test_pull_refused_by_the_stream_engines():
-    """MPX_XFER_PULL is a kernel-engine mode: the SDMA engine refuses it."""
-    P = Pairs("sdma", 1, 4096)
+def test_pull_refused_by_the_rccl_engine():
+    """MPX_XFER_PULL is a kernel / SDMA engine mode: RCCL (a rank paired with
+    itself, the form one GPU runs) refuses it."""
+    c = mpx.Context(1, "rccl")
     try:
-        out, errs = P.run(mpx.MODE_PINGPONG, 4096, 1, pull=True, ranks=[0])
-        assert errs[0].status == mpx.ERR_UNSUPPORTED, errs
+        tx, rx = c.alloc(0, 4096), c.alloc(0, 4096)
+        c.attach(0, 0, tx, rx, 4096)
+        c.rccl_init_all()
+        with pytest.raises(mpx.MpxError) as e:
+            c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, 1, tx, rx, 4096, pull=True)
+        assert e.value.status == mpx.ERR_UNSUPPORTED
     finally:
-        P.close()
+        c.close()
 
 
-def test_pull_timeout_when_peer_never_runs():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_pull_timeout_when_peer_never_runs(engine):
     """A receiver whose peer never publishes gives up at its deadline, like a
     push receiver; so does a sender whose peer never loads."""
-    P = Pairs("kernel", 1, 65536)
+    P = Pairs(engine, 1, 65536)
     try:
         out, errs = P.run(mpx.MODE_PINGPONG, 65536, 3, timeout_ms=300, ranks=[1], pull=True)   # G0 waits
         assert errs[1].status == mpx.ERR_TIMEOUT, errs
     finally:
         P.close()
-    P = Pairs("kernel", 1, 65536)
+    P = Pairs(engine, 1, 65536)
     try:
         out, errs = P.run(mpx.MODE_UNIDIR, 65536, 3, timeout_ms=300, ranks=[0], pull=True)     # G1 waits
         assert errs[0].status == mpx.ERR_TIMEOUT, errs
@@ -263,9 +289,10 @@ def test_pull_timeout_when_peer_never_runs():
         P.close()
 
 
-def test_pull_check_detects_a_wrong_expectation():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_pull_check_detects_a_wrong_expectation(engine):
     """Tell one receiver to expect another payload: every iteration fails."""
-    P = Pairs("kernel", 1, 65536)
+    P = Pairs(engine, 1, 65536)
     try:
         out, errs = {}, {}
 

@@ -121,16 +121,16 @@ GPU_CASES = ["pingpong_p1_b1_i10", "pingpong_p1_b456131_i3", "unidir_p1_b8_i10",
 
 
 def engine_env(engine: str) -> dict:
-    """the binding's engine (MPX_ENGINE); "kernel-pull": the kernel engine
-    with every B-byte payload pulled by its receiver (MPX_XFER_PULL=1)"""
-    if engine == "kernel-pull":
-        return {"MPX_ENGINE": "kernel", "MPX_XFER_PULL": "1"}
+    """the binding's engine (MPX_ENGINE); "<engine>-pull": that engine with
+    every B-byte payload pulled by its receiver (MPX_XFER_PULL=1)"""
+    if engine.endswith("-pull"):
+        return {"MPX_ENGINE": engine[:-len("-pull")], "MPX_XFER_PULL": "1"}
     return {"MPX_ENGINE": engine}
 
 
 @pytest.mark.gpu
 @needs_bin
-@pytest.mark.parametrize("engine", ["kernel", "sdma", "kernel-pull"])
+@pytest.mark.parametrize("engine", ["kernel", "sdma", "kernel-pull", "sdma-pull"])
 @pytest.mark.parametrize("case", GPU_CASES)
 def test_patched_reference_receives_match_reference(tmp_path, case, engine):
     c = GOLDEN[case]

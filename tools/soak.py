@@ -9,7 +9,7 @@ mode every payload is checksummed on the device.
     python tools/soak.py procs <calls> <seed> [engine]     two processes over IPC
     python tools/soak.py worker <dir> <rank> <calls> <seed> <engine>   (one process of `procs`)
 
-engine: kernel (default; push and pull calls) or sdma (push only).  With a
+engine: kernel (default) or sdma; both with push and pull calls.  With a
 negative-control knob set (MPX_TEST_NO_POSTED=1, MPX_TEST_NO_PULL_WAIT=1) the
 soak must report failures: that is what shows it can see the races.
 
@@ -44,7 +44,7 @@ def plan(calls, seed, engine="kernel"):
             iters = rng.choice([1, 2, 17, 255, 256, 257, 300]) if n <= (1 << 20) else rng.randint(1, 20)
         else:
             iters = rng.randint(1, 40) if n <= (1 << 20) else rng.randint(1, 8)
-        pull = rng.random() < 0.5 and engine == "kernel"
+        pull = rng.random() < 0.5
         out.append(dict(mode=mode, n=n, iters=iters, check=rng.random() < 0.6, pull=pull,
                         nwg=rng.choice([0, 0, 1, 3, 8, 64, 128, 256]), stream=rng.random() < 0.3,
                         refill=rng.random() < 0.2, key=rng.getrandbits(32)))
