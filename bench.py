@@ -534,14 +534,16 @@ def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict
 
 
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                latency=True, tune=True) -> dict:
-    """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers).
+                latency=True, tune=True, pull=False) -> dict:
+    """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers;
+    pull: the engine's MPX_XFER_PULL form, validation and steps alike).
     Every round's payloads are validated once (check mode, seeded per-rank
     patterns) before anything is timed.  Returns a dict; "error" is set (on
     every rank) if any rank failed."""
     rounds = all_pairs_rounds(world)
     out = {}
     c = None
+    pkw = {"pull": True} if pull else {}   # (the keyword only when set: the default call stays as it was)
 
     def agree(err: str) -> str:
         """every rank learns the first error of any rank (one gloo collective)"""
@@ -589,7 +591,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
                 continue
             try:
                 c.xfer(mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True,
-                       expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000)
+                       expect=descs[peer][1], expect_ack=descs[peer][2], timeout_ms=10000, **pkw)
             except Exception as e:  # noqa: BLE001
                 err = f"rank {rank}: round {r}: {type(e).__name__}: {e}"[:300]
         err = agree(err)
@@ -625,7 +627,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         if step_err:                                 # keep joining the barriers, transfer nothing
             return g, None
         try:
-            return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream)
+            return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream, **pkw)
         except Exception as e:  # noqa: BLE001
             step_err.append(f"rank {rank}: step {s}: {type(e).__name__}: {e}"[:300])
             return g, None
@@ -637,7 +639,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     if engine == "sdma":
         for r in range(len(rounds)):
             g, peer = round_role(rounds, r, rank)
-            c.prepare(mpx.MODE_UNIDIR, g, rank, peer, iters, nbytes)
+            c.prepare(mpx.MODE_UNIDIR, g, rank, peer, iters, nbytes, **pkw)
     for s in range(max(warmup, len(rounds))):
         step(s)
     dev_s, n_sends = 0.0, 0
@@ -994,6 +996,14 @@ def main() -> None:
             extras[f"{eng}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
             # every round's payloads checksummed on this engine before timing (BASELINE config 5)
             extras[f"{eng}_validated_rounds"] = r2.get("validated_rounds", 0)
+        # the pulled forms of the kernel and SDMA engines over the same rounds
+        # (MPX_XFER_PULL: the receiver loads / its stream copies the
+        # sender's tx), every round validated first
+        for eng in ("kernel", "sdma"):
+            r4 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
+                             latency=False, tune=False, pull=True)
+            extras[f"{eng}_pull_aggregate_GBps"] = r4.get("error") or round(r4["total"] / r4["elapsed"] / 1e9, 3)
+            extras[f"{eng}_pull_validated_rounds"] = r4.get("validated_rounds", 0)
         with lock:
             done.set()
         dog.cancel()

@@ -236,10 +236,11 @@ class Context:
         return t
 
     def prepare(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, length: int,
-                timeout_ms: int = 0) -> None:
-        """mpx_xfer_prepare: before timing, build the SDMA engine's graph chunks or
-        set up the RCCL engine's channel to peer_rank (both ranks call it)"""
-        o = XferOpts(timeout_ms=timeout_ms)
+                timeout_ms: int = 0, pull: bool = False) -> None:
+        """mpx_xfer_prepare: before timing, build the SDMA engine's graph chunks
+        (pull: its pulled form's) or set up the RCCL engine's channel to
+        peer_rank (both ranks call it)"""
+        o = XferOpts(timeout_ms=timeout_ms, flags=XFER_PULL if pull else 0)
         check(self.L.mpx_xfer_prepare(self.h, mode, group, my_rank, peer_rank, iters, length, C.byref(o)),
               "mpx_xfer_prepare")
 

@@ -107,8 +107,8 @@ class FakeMpx:
                 return Timing(ms * 1e-3, ms * 1e-3)
             return Timing(0.002, 0.001 * (1 + me))
 
-        def prepare(self, mode, group, me, peer, iters, n, timeout_ms=0):
-            FakeMpx.log.append(["prepare", self.engine, mode, group, me, peer, iters, n])
+        def prepare(self, mode, group, me, peer, iters, n, timeout_ms=0, pull=False):
+            FakeMpx.log.append(["prepare", self.engine, mode, group, me, peer, iters, n, pull])
 
         def close(self):
             FakeMpx.log.append(["close", self.engine])

@@ -48,6 +48,9 @@ def test_one_json_line_with_the_contract_keys():
     assert d["config"]["workload"] == "all_pairs_rounds_unidir" and d["config"]["engine"] == "kernel"
     assert d["roofline"]["bound"] == "xgmi" and d["roofline"]["peak"] == 76.8
     assert isinstance(d["extras"]["sdma_aggregate_GBps"], float)
+    # the pulled forms of the kernel and SDMA engines over the same rounds
+    assert isinstance(d["extras"]["kernel_pull_aggregate_GBps"], float), d["extras"]
+    assert isinstance(d["extras"]["sdma_pull_aggregate_GBps"], float)
     assert isinstance(d["extras"]["rccl_aggregate_GBps"], float)
     # the comparison engines checksum every round before timing it (config 5)
     assert d["extras"]["sdma_validated_rounds"] == 1 and d["extras"]["rccl_validated_rounds"] == 1
