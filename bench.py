@@ -987,23 +987,25 @@ def main() -> None:
                 extras["unidir_64MiB_per_pair_GBps"] = round(r3["per_pair_GBps"], 2)
                 extras["unidir_64MiB_pair_GBps_min_max"] = r3.get("pair_GBps_min_max")
                 extras["headline_over_64MiB"] = round(achieved / r3["per_pair_GBps"], 4)
-        for eng in ("sdma", "rccl"):
-            if config["engine"].startswith(eng):
+        # RCCL last: on the one-GPU rehearsal its (refused) communicator init
+        # leaves every process with more streams than the card has hardware
+        # queues, and the co-dependent halves of a pair then share time
+        # slices — every later round ran ~1000x slower there
+        # (profiles/r03_pull_rounds_diag.jsonl)
+        for eng, pull in (("sdma", False), ("kernel", True), ("sdma", True), ("rccl", False)):
+            if not pull and config["engine"].startswith(eng):
                 continue
             # 512 iterations: two graph-replayed SDMA chunks (run_sdma), no host-bound tail
             r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
-                             latency=False)
-            extras[f"{eng}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
-            # every round's payloads checksummed on this engine before timing (BASELINE config 5)
-            extras[f"{eng}_validated_rounds"] = r2.get("validated_rounds", 0)
-        # the pulled forms of the kernel and SDMA engines over the same rounds
-        # (MPX_XFER_PULL: the receiver loads / its stream copies the
-        # sender's tx), every round validated first
-        for eng in ("kernel", "sdma"):
-            r4 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
-                             latency=False, tune=False, pull=True)
-            extras[f"{eng}_pull_aggregate_GBps"] = r4.get("error") or round(r4["total"] / r4["elapsed"] / 1e9, 3)
-            extras[f"{eng}_pull_validated_rounds"] = r4.get("validated_rounds", 0)
+                             latency=False, tune=False, pull=pull) if pull else \
+                pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
+                            latency=False)
+            # every round's payloads checksummed on this engine before timing
+            # it (BASELINE config 5); pull: the engine's MPX_XFER_PULL form
+            # (the receiver loads / its stream copies the sender's tx)
+            key = f"{eng}_pull" if pull else eng
+            extras[f"{key}_aggregate_GBps"] = r2.get("error") or round(r2["total"] / r2["elapsed"] / 1e9, 3)
+            extras[f"{key}_validated_rounds"] = r2.get("validated_rounds", 0)
         with lock:
             done.set()
         dog.cancel()
