@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 5
+#define MPX_ABI_VERSION 6
 #define MPX_MAX_RANKS 64          /* ranks one context can address           */
 #define MPX_RANK_DESC_BYTES 512   /* size of the opaque exported descriptor  */
 #define MPX_RCCL_ID_BYTES 128     /* size of an RCCL unique id               */
@@ -152,6 +152,14 @@ typedef struct mpx_xfer_opts {
    (MPX_ERR_UNSUPPORTED).  The environment variable MPX_XFER_PULL=1 makes it
    the kernel and SDMA engines' default. */
 #define MPX_XFER_PULL 2
+/* mpx_xfer_opts.flags: kernel engine, bulk pushes read tx from HBM at every
+   push instead of from the LDS copy each pushing workgroup takes once per
+   call (the default whenever a workgroup's chunk fits in LDS, <= 60 KiB: tx
+   is read-only while the loop runs, and the reference re-sends the same
+   buffer every iteration, mpi_perf.c:72,80,136).  The link bytes are the
+   same either way; this flag shows that the staged figure is not an LDS
+   artefact (bench.py extras.unidir_4MiB_unstaged_GBps). */
+#define MPX_XFER_NOSTAGE 4
 
 /* opaque context */
 typedef struct mpx_ctx mpx_ctx;
@@ -171,6 +179,10 @@ int mpx_device_count(int *count);
 #define MPX_LINK_PCIE 2
 #define MPX_LINK_XGMI 4
 int mpx_link_info(int dev_a, int dev_b, int *link_type, int *hops);
+/* PCI bus id of a visible GPU ("DDDD:BB:DD.F", hipDeviceGetPCIBusId) — how
+   hosts name a GPU to tools that address devices by bus (the counters of
+   include/mpxprof.h); len >= 16 */
+int mpx_device_bus_id(int dev, char *buf, int len);
 
 /* MPI_Init analogue (mpi_perf.c:372): a context able to address `nranks`
    ranks (<= MPX_MAX_RANKS) with the given engine. */
@@ -238,6 +250,27 @@ int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank
    engine. */
 int mpx_xfer_prepare(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
                      int buff_len, const mpx_xfer_opts *opts);
+
+/* Where the last kernel-engine call of a local rank spent its wall time.
+   The reference times the loop with MPI_Wtime around it (mpi_perf.c:501,
+   532-533); a GPU loop adds a launch before the kernel runs and a
+   completion after, which short loops (run-hbv3.sh: -i 10) pay per call.
+   Kernel-side times come from the kernel's own clock (s_memrealtime), host-
+   side ones from CLOCK_MONOTONIC; launch_to_start_s and done_to_return_s
+   are 0 when the call waited with MPX_SYNC=event. */
+typedef struct mpx_phases {
+    double wall_s;            /* the call's mpx_timing.wall_s                   */
+    double host_prep_s;       /* call entry -> launch (argument set-up)         */
+    double launch_to_start_s; /* launch -> the kernel's first workgroup runs
+                                 (completion word seen - launch - kernel_s)     */
+    double posted_wait_s;     /* kernel start -> the peer's receives are posted
+                                 (sides that push first; includes the peer's
+                                 own late start)                                */
+    double kernel_s;          /* first workgroup start -> last workgroup end    */
+    double done_to_return_s;  /* completion word seen -> the kernel retired and
+                                 the call returned                              */
+} mpx_phases;
+int mpx_last_phases(mpx_ctx *ctx, int rank, mpx_phases *out);
 
 /* MPI_Barrier analogue (mpi_perf.c:499,557,579) for the threads of ONE
    process: blocks until `nthreads` callers have entered with the same ctx.

@@ -70,9 +70,18 @@ struct Status {
     u64 recv_digest;        // check mode: sum of their finished checksums
     u64 seen, want;         // stream engines: flag value seen / awaited by the
                             // wait that timed out (diagnostics)
+    // kernel engine, phases of the last call (s_memrealtime, 100 MHz ticks):
+    u64 t_entry;            // workgroup 0 started
+    u64 t_posted;           // this side may push: the peer's receives are
+                            // posted (0: this side pushes only after a receive)
+    u64 t_exit;             // the last workgroup finished
+    u64 done;               // XferArgs.done_token, stored by the last workgroup
+                            // after everything else (the host's completion word)
 };
 
-// Device scratch words of a rank (zeroed per kernel-engine call, [0..3]):
+// Device scratch words of a rank ([0..3]: zero when a kernel-engine call
+// starts — zeroed at attach, and reset by the last workgroup of every call, so
+// no memset precedes the launch):
 //   [0] grid-barrier counter  [1] abort word  [2] finished workgroups
 //   [3] pull mode: chunks landed in rx this call (all receives, all workgroups)
 //   [4..5] SDMA engine's device-side sequence base {tx, rx}
@@ -112,8 +121,6 @@ struct XferArgs {
     int peer_slot;               // peer rank = its slot in my mailbox
     int nwg;                     // bulk push workgroups (same on both sides)
     int check;                   // 1 = checksum + poison each received payload
-    int ll_flags;                // bit2: re-read tx at every LL send (A/B of the
-                                 //       register-held payload); other bits unused
     int ll_max;                  // messages <= ll_max bytes use LL (<= kLLMaxBytes);
                                  // same on both sides of the link
     int stream;                  // 1: bulk payload stores add the nt hint (sc0 sc1 nt)
@@ -139,6 +146,7 @@ struct XferArgs {
     int pull;                    // 1 = this call's bulk payloads are pulled
     int no_pull_wait;            // test knob (MPX_TEST_NO_PULL_WAIT): a sending side
                                  // ends without waiting for the peer's loads of tx
+    u64 done_token;              // stored into Status.done by the last workgroup
 };
 
 // LL threshold of a link.  Within one GPU the bulk path's extra hop (payload
@@ -197,12 +205,12 @@ constexpr size_t kCopyStepsDefaultMax = (size_t)1 << 20;
 constexpr size_t kCopyPipeDefaultMin = (size_t)512 << 10;
 constexpr size_t kCopyPipeDefaultMax = (size_t)16 << 20;
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
-                             int* grid_out);
+                             int* grid_out, const int* shape = nullptr);
 // all `iters` copies in one k_copy_pipe launch (copy s+1's loads in flight
 // across copy s's grid barrier, a dedicated barrier wave); *bar must be 0
 constexpr int kCopyPipeMaxGrid = 768;     // 320-lane workgroups, 3 per CU: resident
 hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
-                            int* grid_out);
+                            int* grid_out, int upl_force = 0, int hier_force = -1);
 hipError_t launch_fill(void* p, size_t n, int pattern, u64 arg, hipStream_t s);
 hipError_t launch_checksum(const void* p, size_t n, u64* out_dev, hipStream_t s);
 hipError_t launch_signal(u64* flag, const u64* base, u64 value, hipStream_t s);

@@ -73,8 +73,7 @@ __device__ __forceinline__ u64 block_sum(u64 v, u64* lds4) {
 //   CONTIG = false: grid-stride over the whole buffer (unit i, i+G, ...)
 //   CONTIG = true : block b owns one contiguous chunk, swept 4 KiB per step
 //   LDNT / STNT   : nontemporal (streaming) loads / stores
-// The variant is chosen at launch (launch_copy; MPX_COPY_VARIANT overrides
-// for tuning sweeps).
+// launch_copy runs one form: U = 1, nontemporal both ways, one step per block.
 // ---------------------------------------------------------------------------
 template <bool NT>
 __device__ __forceinline__ v4u ld16(const v4u* p) {
@@ -240,6 +239,10 @@ constexpr int kAuxNt = 2;                                 // buffer op: nt (stre
 __device__ __forceinline__ void wg_barrier_nofence() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS (s_stop) before the barrier
     __builtin_amdgcn_s_barrier();
+    // LLVM models s_barrier as touching no memory: without a compiler barrier
+    // after it too, the s_stop read or the next copy's stores could be
+    // scheduled above it
+    asm volatile("" ::: "memory");
 }
 
 // Branch-free copy-wave code: every unit is a buffer op whose resource ends at
@@ -690,6 +693,7 @@ struct Loop {
                 __builtin_amdgcn_s_sleep(1);
             }
         }
+        stamp(&a.status->t_posted);
         __syncthreads();
         return !aborted();
     }
@@ -765,14 +769,7 @@ struct Loop {
     // blocking Recv).  At the end the last workgroup to finish (all chunk
     // checksums are in by then) adds up the finished checksums of the `done`
     // receives (check mode) and stores the count and digest.
-    __device__ void account_all(u64 done, long long n_recv) const {
-        __shared__ int s_last;
-        __syncthreads();
-        if (threadIdx.x == 0)
-            s_last = __hip_atomic_fetch_add(&a.gbar[kScrFin], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-                     (u64)gridDim.x - 1;
-        __syncthreads();
-        if (!s_last) return;
+    __device__ void account(u64 done, long long n_recv) const {
         u64 part = 0;
         if (a.check) {
             const u64 fmix = mix64((u64)n_recv);
@@ -784,6 +781,38 @@ struct Loop {
             __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&a.status->recv_digest, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+    }
+
+    // ---- call phases and the end of the call --------------------------------
+    // Workgroup 0 stamps the call's start (Status.t_entry) as its first action
+    // and, on a side that pushes first, the moment the peer's receives were
+    // seen posted (t_posted): the host splits a call's wall time into launch,
+    // wait for the peer, transfer and completion with them (mpx_last_phases).
+    __device__ void stamp(u64* field) const {
+        if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(field, now_ticks());
+    }
+    // Every workgroup calls it last; true (uniformly) in the one that
+    // finishes last — every other workgroup is done with the scratch words
+    // and the status fields by then.
+    __device__ bool last_to_finish() const {
+        __shared__ int s_last;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            s_last = __hip_atomic_fetch_add(&a.gbar[kScrFin], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (u64)gridDim.x - 1;
+        __syncthreads();
+        return s_last != 0;
+    }
+    // The last workgroup: scratch words [0..3] back to zero for the rank's
+    // next call (so no memset precedes a launch), the call's exit time, then
+    // — after every status store of the call has drained — the completion
+    // word the host spins on (Status.done = this call's token).
+    __device__ void finish_last() const {
+        if (threadIdx.x != 0) return;
+        for (int k = 0; k < 4; ++k) __hip_atomic_store(&a.gbar[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sys(&a.status->t_exit, now_ticks());
+        drain_stores();
+        st_sys(&a.status->done, a.done_token);
     }
 
     // ---- non-blocking check mode (k_xfer_nbcheck) ----------------------------
@@ -1050,6 +1079,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     extern __shared__ v4u s_tx[];            // a.stage: dynamic LDS = one chunk
     if (threadIdx.x == 0) s_abort = 0;
     Loop<MODE> L{a, &s_abort, lds4, s_tx, {}};
+    L.stamp(&a.status->t_entry);
     const long long n = a.len;
     if (a.stage) L.stage_tx(n);
     __syncthreads();
@@ -1057,7 +1087,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     const long long send_len = (MODE == MPX_MODE_UNIDIR && GROUP == 0) ? 1 : n;
     const bool ll_send = blockIdx.x == 0 && L.is_ll(send_len);
     if (ll_send) L.preload_ll(send_len);
-    const bool reload = ll_send && (a.ll_flags & 4);   // A/B knob (bit 2): re-read tx at every send
     u64 txs = a.tx_seq0, rxs = a.rx_seq0;
     u64 done = 0;                                       // receives completed (Status.recv_done)
     int inflight = 0;
@@ -1071,7 +1100,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
         const bool skip = a.skip_push == i + 1;        // test knob only
         if constexpr (MODE == MPX_MODE_PINGPONG) {    // mpi_perf.c:70-82
             if constexpr (GROUP == 1) {
-                if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs, skip);                // Send(tx, B, tag 1)
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 2)
                 ++done;
@@ -1080,12 +1108,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 1)
                 ++done;
                 if (a.check) L.check(n, i);
-                if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs, skip);                // Send(tx, B, tag 2)
             }
         } else if constexpr (MODE == MPX_MODE_UNIDIR) {  // mpi_perf.c:132-144
             if constexpr (GROUP == 1) {
-                if (reload) L.preload_ll(send_len);
                 L.send(n, ++txs, skip);                // Send(tx, B)
                 if (!L.recv(1, ++rxs, i)) break;       // Recv(rx, 1) — the ack
                 ++done;
@@ -1094,7 +1120,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B)
                 ++done;
                 if (a.check) { L.check(n, i); if (!L.grid_sync(i)) break; }
-                if (reload) L.preload_ll(send_len);
                 L.send(1, ++txs, skip);                // Send(tx, 1)
             }
         } else {                                       // mpi_perf.c:95-124
@@ -1125,8 +1150,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
             done += (u64)inflight;
         if (blockIdx.x == 0 && threadIdx.x == 0)
             __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-        L.account_all(done, (MODE == MPX_MODE_UNIDIR && GROUP == 1) ? 1 : n);
+        if (L.last_to_finish()) L.finish_last();
+    } else if (L.last_to_finish()) {
+        L.account(done, (MODE == MPX_MODE_UNIDIR && GROUP == 1) ? 1 : n);
+        L.finish_last();
     }
 }
 
@@ -1148,6 +1175,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     extern __shared__ v4u s_tx[];
     if (threadIdx.x == 0) s_abort = 0;
     Loop<MPX_MODE_NONBLOCKING> L{a, &s_abort, lds4, s_tx, {}};
+    L.stamp(&a.status->t_entry);
     const long long n = a.len;
     if (a.stage) L.stage_tx(n);
     __syncthreads();
@@ -1164,6 +1192,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     // call's last credits already satisfy this call's first S pushes.
     L.post_receives();
     bool ok = a.iters == 0 || L.nb_wait([&] { return threadIdx.x != 0 || L.peer_posted(); }, &next, 0);
+    L.stamp(&a.status->t_posted);
     for (int i = 0; i < a.iters && ok; ++i) {
         // slot ring_slot(i) was last used by push i - S of this call: wait
         // for its credit
@@ -1191,6 +1220,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
         __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.status->recv_digest, dig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (L.last_to_finish()) L.finish_last();
 }
 
 // k_xfer_pull: the three loops with every B-byte payload PULLED by its
@@ -1216,6 +1246,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
         s_seen = 0;
     }
     Loop<MODE> L{a, &s_abort, lds4, nullptr, {}, &s_seen};
+    L.stamp(&a.status->t_entry);
     const long long n = a.len;
     const u64 nw = (u64)a.nwg;
     if (MODE == MPX_MODE_UNIDIR && GROUP == 0 && blockIdx.x == 0) L.preload_ll(1);   // the ack's byte
@@ -1275,23 +1306,26 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
         // final Waitall(inflight); then workgroup 0 counts and digests the
         // receives the reference waits for (all but slot 255 of each full
         // window)
-        if (blockIdx.x != 0) return;
-        if (ok && a.iters > 0) ok = L.template poll_ge<false>(&a.gbar[kScrLanded], nw * (u64)a.iters, a.iters - 1);
-        if (ok) done += (u64)inflight;
-        u64 part = 0;
-        if (ok && a.check) {
-            const u64 fmix = mix64((u64)n);
-            for (int j = threadIdx.x; j < a.iters; j += kBlock)
-                if (j % kNbWindow != kNbWindow - 1)
-                    part += __hip_atomic_load(&a.csum[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ fmix;
+        if (blockIdx.x == 0) {
+            if (ok && a.iters > 0) ok = L.template poll_ge<false>(&a.gbar[kScrLanded], nw * (u64)a.iters, a.iters - 1);
+            if (ok) done += (u64)inflight;
+            u64 part = 0;
+            if (ok && a.check) {
+                const u64 fmix = mix64((u64)n);
+                for (int j = threadIdx.x; j < a.iters; j += kBlock)
+                    if (j % kNbWindow != kNbWindow - 1)
+                        part += __hip_atomic_load(&a.csum[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ fmix;
+            }
+            const u64 s = block_sum(part, lds4);
+            if (threadIdx.x == 0) {
+                __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&a.status->recv_digest, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
-        const u64 s = block_sum(part, lds4);
-        if (threadIdx.x == 0) {
-            __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&a.status->recv_digest, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    } else {
-        L.account_all(done, (MODE == MPX_MODE_UNIDIR && GROUP == 1) ? 1 : n);
+        if (L.last_to_finish()) L.finish_last();
+    } else if (L.last_to_finish()) {
+        L.account(done, (MODE == MPX_MODE_UNIDIR && GROUP == 1) ? 1 : n);
+        L.finish_last();
     }
 }
 
@@ -1338,67 +1372,29 @@ hipError_t launch_xfer(const XferArgs& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-typedef void (*copy_fn)(const v4u*, v4u*, size_t, unsigned);
-
-#define COPY_VARIANTS(U)                                                                            \
-    {U, 0, 0, 0, k_copy<U, false, false, false>}, {U, 1, 0, 0, k_copy<U, true, false, false>},     \
-    {U, 0, 1, 0, k_copy<U, false, true, false>},  {U, 1, 1, 0, k_copy<U, true, true, false>},      \
-    {U, 0, 0, 1, k_copy<U, false, false, true>},  {U, 1, 0, 1, k_copy<U, true, false, true>},      \
-    {U, 0, 1, 1, k_copy<U, false, true, true>},   {U, 1, 1, 1, k_copy<U, true, true, true>}
-
-struct CopyVariant {
-    int u, ldnt, stnt, contig;
-    copy_fn fn;
-};
-static const CopyVariant kCopyVariants[] = {COPY_VARIANTS(1), COPY_VARIANTS(2), COPY_VARIANTS(4), COPY_VARIANTS(8),
-                                            COPY_VARIANTS(16)};
-
-// Default from the tuning sweeps (DESIGN.md "k_copy tuning"): ONE 16-B unit
-// per lane and ONE step per block — grid = n/4 KiB workgroups of 256 lanes,
-// no cap (blocks_per_cu = 0), nontemporal loads and stores.  6.51-6.53 TB/s
-// of HBM traffic at 256 MiB, 1 GiB and 4 GiB alike (profiles/
-// r01_copy_lab_onestep.jsonl), against 6.0 / 5.45 TB/s for the earlier
-// contiguous-chunk form (2 loads per lane, 16 KiB per block, 65536 blocks)
-// and 4.76 TB/s for hipMemcpyAsync device-to-device.
-struct CopyConfig {
-    int u = 1, ldnt = 1, stnt = 1, contig = 0, blocks_per_cu = 0;
-};
-
-static CopyConfig copy_config() {
-    CopyConfig c;
-    // MPX_COPY_VARIANT="U:ldnt:stnt:contig:blocks_per_cu"
-    if (const char* v = getenv("MPX_COPY_VARIANT")) {
-        int a[5];
-        if (sscanf(v, "%d:%d:%d:%d:%d", &a[0], &a[1], &a[2], &a[3], &a[4]) == 5) {
-            c.u = a[0]; c.ldnt = a[1]; c.stnt = a[2]; c.contig = a[3]; c.blocks_per_cu = a[4];
-        }
-    }
-    return c;
-}
-
+// One k_copy form, from the tuning sweeps (DESIGN.md "k_copy tuning"): ONE
+// 16-B unit per lane and ONE step per block — grid = n/4 KiB workgroups of
+// 256 lanes, no cap, nontemporal loads and stores.  6.51-6.53 TB/s of HBM
+// traffic at 256 MiB, 1 GiB and 4 GiB alike (profiles/r01_copy_lab_onestep.jsonl),
+// against 6.0 / 5.45 TB/s for the earlier contiguous-chunk form and 4.76 TB/s
+// for hipMemcpyAsync device-to-device.  The 39 other instantiations of round
+// 1-3's variant knob (unroll x load/store policy x layout) are gone; their
+// evidence stays in profiles/copy_sweep_r01.jsonl and r01_copy_policy_*.
 hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t s, int* grid_out) {
-    static const CopyConfig cfg = copy_config();
-    copy_fn fn = nullptr;
-    for (const CopyVariant& v : kCopyVariants)
-        if (v.u == cfg.u && v.ldnt == cfg.ldnt && v.stnt == cfg.stnt && v.contig == cfg.contig) fn = v.fn;
-    if (!fn) return hipErrorInvalidValue;
     const size_t n16 = n / 16;
     const unsigned tail = (unsigned)(n & 15);
-    size_t grid = (n16 + (size_t)kBlock * cfg.u - 1) / ((size_t)kBlock * cfg.u);
-    // blocks_per_cu = 0: one step per block (grid-stride loops then run once);
-    // the cap only bounds gridDim.x, which a 2^31-unit copy stays far below
-    const size_t cap = cfg.blocks_per_cu > 0 ? (size_t)256 * cfg.blocks_per_cu : ((size_t)1 << 30);
-    if (grid > cap) grid = cap;
+    size_t grid = (n16 + (size_t)kBlock - 1) / (size_t)kBlock;
     if (grid < 1) grid = 1;
+    if (grid > ((size_t)1 << 31) - 1) return hipErrorInvalidValue;
     if (grid_out) *grid_out = (int)grid;
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kBlock), 0, s, reinterpret_cast<const v4u*>(src),
-                       reinterpret_cast<v4u*>(dst), n16, tail);
+    hipLaunchKernelGGL((k_copy<1, true, true, false>), dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       reinterpret_cast<const v4u*>(src), reinterpret_cast<v4u*>(dst), n16, tail);
     return hipGetLastError();
 }
 
 hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
-                             int* grid_out) {
+                             int* grid_out, const int* shape) {
     // Defaults from the A/Bs: at most 64 workgroups and one hot counter
     // (fewer arrivals beat more lanes: 1 MiB 2.08 us vs 2.40 with 256,
     // profiles/r02_copy_steps_variants.jsonl); no store drain before arrival
@@ -1416,11 +1412,11 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
     // with 8 units per lane, all loads of a step in flight at once: 2 MiB
     // 2.35 us against 2.56-3.07 with 1024 lanes x 2
     // (r02_copy_steps_wgsize_mid.jsonl, r02_copy_sweep_state.jsonl).
+    // `shape` (tests only: MPX_COPY="steps:..." via mpx_copy) overrides
+    // {grid_cap, xcd, drain, upl, threads, one_xcd}.
     // Default-policy loads instead of nontemporal ones change nothing here,
     // fresh or after 1 GiB copies evicted src (r02_copy_steps_ldpolicy.jsonl,
     // measured with a knob since removed).
-    // MPX_COPY_STEPS="grid_cap:xcd:drain:upl:threads:one_xcd" overrides (A/B
-    // knobs, read per call; threads = lanes per workgroup, 256 / 512 / 1024).
     // One XCD: from 32 KiB to 512 KiB every working workgroup sits on XCD 0
     // (8x the grid, the others exit at once), so the barrier's arrivals stay
     // within one XCD: 32-64 KiB 1.16-1.20 -> 1.02 us per copy (512 lanes),
@@ -1435,8 +1431,9 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
         threads = kBlock;
         upl = 8;
     }
-    if (const char* v = getenv("MPX_COPY_STEPS"))
-        sscanf(v, "%d:%d:%d:%d:%d:%d", &cap, &xcd, &drain, &upl, &threads, &one_xcd);
+    if (shape) {
+        cap = shape[0]; xcd = shape[1]; drain = shape[2]; upl = shape[3]; threads = shape[4]; one_xcd = shape[5];
+    }
     if (threads != 512 && threads != 1024) threads = kBlock;
     // the grid barrier needs every workgroup resident: at most the waves of
     // kCopyStepsMaxGrid 256-lane workgroups (4 per CU), whatever the width
@@ -1467,7 +1464,7 @@ hipError_t launch_copy_steps(void* dst, const void* src, size_t n, int iters, u6
 // the grid (<= kCopyPipeMaxGrid workgroups of 320 lanes, all resident) covers
 // n; returns hipErrorInvalidValue when n is too large for a resident grid.
 hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64* bar, hipStream_t s,
-                            int* grid_out) {
+                            int* grid_out, int upl_force, int hier_force) {
     const size_t n16 = n / 16;
     const size_t lanes = (size_t)kPipeCopyWaves * 64;
     // resident grid: 5-wave workgroups, as many per CU as the VGPRs allow
@@ -1487,8 +1484,7 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     const bool big = n > ((size_t)1 << 20);
     int upl = big ? 4 : 8;
     while (big && upl < 16 && (n16 + lanes * upl - 1) / (lanes * upl) > 256) upl *= 2;
-    if (const char* v = getenv("MPX_COPY_PIPE_UPL"))   // A/B knob, read per call
-        if (*v) upl = atoi(v);
+    if (upl_force > 0) upl = upl_force;   // tests: every units-per-lane form
     upl = upl <= 1 ? 1 : upl <= 2 ? 2 : upl <= 4 ? 4 : upl <= 8 ? 8 : 16;
     size_t grid = (n16 + lanes * upl - 1) / (lanes * upl);
     while (grid > cap_of(upl) && upl < 16) {
@@ -1503,9 +1499,7 @@ hipError_t launch_copy_pipe(void* dst, const void* src, size_t n, int iters, u64
     void (*k)(const v4u*, v4u*, size_t, unsigned, int, u64*, int) =
         upl <= 1 ? k_copy_pipe<1> : upl <= 2 ? k_copy_pipe<2> : upl <= 4 ? k_copy_pipe<4>
         : upl <= 8 ? k_copy_pipe<8> : k_copy_pipe<16>;
-    int hier = big ? 1 : 0;   // MPX_COPY_PIPE_HIER=0|1 forces the barrier form (A/B knob, read per call)
-    if (const char* v = getenv("MPX_COPY_PIPE_HIER"))
-        if (*v) hier = atoi(v) != 0;
+    const int hier = hier_force >= 0 ? (hier_force != 0) : (big ? 1 : 0);   // tests: both barrier forms
     (void)hipGetLastError();   // drop a stale error of an earlier, ignored call
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kPipeThreads), 0, s, reinterpret_cast<const v4u*>(src),
                        reinterpret_cast<v4u*>(dst), n16, (unsigned)(n & 15), iters, bar, hier);

@@ -109,6 +109,8 @@ struct Rank {
     int mb_kind = kMbUncached;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    u64 token = 0;                 // kernel-engine calls made: Status.done of the last one
+    mpx_phases phases{};           // the last kernel-engine call (mpx_last_phases)
     Status* status = nullptr;      // host-mapped (local ranks)
     u64* scratch = nullptr;        // kScratchWords device words (local ranks)
     u64* csum = nullptr;           // per-iteration checksums (device), csum_cap words,
@@ -199,15 +201,9 @@ int check_dev(int dev) {
 // Allocate the rank's mailbox; prefer uncached device memory (every access
 // goes to memory, so polls see xGMI stores), then fine-grained, then coarse.
 // The kind must also be IPC-exportable for multi-process use.
-// MPX_MAILBOX=uncached|fine|coarse forces one kind (diagnostics).
 int alloc_mailbox(Rank& rk) {
     const unsigned flags[2] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
-    const char* force = getenv("MPX_MAILBOX");
-    int first = 0, last = 1;
-    if (force && !strcmp(force, "fine")) first = 1;
-    if (force && !strcmp(force, "coarse")) first = 2;
-    if (force && !strcmp(force, "uncached")) last = 0;
-    for (int k = first; k <= last; ++k) {
+    for (int k = 0; k <= 1; ++k) {
         void* p = nullptr;
         if (hipExtMallocWithFlags(&p, sizeof(Mailbox), flags[k]) != hipSuccess) {
             (void)hipGetLastError();
@@ -217,12 +213,11 @@ int alloc_mailbox(Rank& rk) {
         const hipError_t e = hipIpcGetMemHandle(&h, p);
         if (getenv("MPX_DEBUG"))
             fprintf(stderr, "[mpx] mailbox kind %d alloc ok, ipc handle: %s\n", k, hipGetErrorString(e));
-        if (e != hipSuccess && !getenv("MPX_MAILBOX")) {
-            (void)hipGetLastError();
+        (void)hipGetLastError();
+        if (e != hipSuccess) {
             (void)hipFree(p);
             continue;
         }
-        (void)hipGetLastError();
         rk.mb = static_cast<Mailbox*>(p);
         rk.mb_kind = k;
         return MPX_OK;
@@ -296,23 +291,38 @@ unsigned char* slot_ptr(const Rank& rk, int j, int iters, int slots, long long l
     return s == 0 ? rk.rx : rk.ring + (long long)(s - 1) * len;
 }
 
-// Largest copy whose iterations run in one k_copy_steps launch
-// (MPX_COPY_STEPS_MAX bytes, read per call for A/B sweeps; 0 = never).
-size_t copy_steps_max() {
-    const char* v = getenv("MPX_COPY_STEPS_MAX");
-    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyStepsDefaultMax;
-}
-
-// Copies of (kCopyPipeDefaultMin, kCopyPipeDefaultMax] bytes run all their
-// iterations in one k_copy_pipe launch (MPX_COPY_PIPE_MIN / MPX_COPY_PIPE_MAX
-// override, read per call; MAX = 0: never).
-size_t copy_pipe_min() {
-    const char* v = getenv("MPX_COPY_PIPE_MIN");
-    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyPipeDefaultMin;
-}
-size_t copy_pipe_max() {
-    const char* v = getenv("MPX_COPY_PIPE_MAX");
-    return v ? (size_t)strtoull(v, nullptr, 0) : (size_t)kCopyPipeDefaultMax;
+// mpx_copy's form.  Default: all copies of a call in one launch where a
+// launch per copy is dispatch-bound — k_copy_steps up to 512 KiB, k_copy_pipe
+// above it to 16 MiB — and a k_copy launch per copy above.
+// MPX_COPY (read per call; the tests drive every form and shape with it):
+//   "launch"                      a k_copy launch per copy, any size
+//   "steps[:cap:xcd:drain:upl:threads:one_xcd]"   k_copy_steps at any size
+//   "pipe[:upl[:hier]]"           k_copy_pipe at any size it can hold
+// Round 3's six copy knobs (MPX_COPY_VARIANT, _STEPS, _STEPS_MAX,
+// _PIPE_MIN, _PIPE_MAX, _PIPE_UPL, _PIPE_HIER) are this one.
+enum CopyForm { kCopyAuto = 0, kCopyLaunch, kCopySteps, kCopyPipe };
+struct CopyChoice {
+    int form = kCopyAuto;
+    bool shaped = false;
+    int shape[6] = {0, 0, 0, 0, 0, 0};   // k_copy_steps: cap, xcd, drain, upl, threads, one_xcd
+    int upl = 0, hier = -1;              // k_copy_pipe
+};
+CopyChoice copy_choice() {
+    CopyChoice c;
+    const char* v = getenv("MPX_COPY");
+    if (!v || !*v) return c;
+    if (!strncmp(v, "launch", 6)) {
+        c.form = kCopyLaunch;
+    } else if (!strncmp(v, "steps", 5)) {
+        c.form = kCopySteps;
+        int* x = c.shape;
+        const int k = sscanf(v + 5, ":%d:%d:%d:%d:%d:%d", &x[0], &x[1], &x[2], &x[3], &x[4], &x[5]);
+        c.shaped = k >= 5;   // one_xcd may be omitted (0)
+    } else if (!strncmp(v, "pipe", 4)) {
+        c.form = kCopyPipe;
+        (void)sscanf(v + 4, ":%d:%d", &c.upl, &c.hier);
+    }
+    return c;
 }
 
 // the receives the reference's non-blocking loop completes (Waitall) for
@@ -322,50 +332,49 @@ u64 nb_waited(int iters) {
     return (u64)iters - (u64)(iters / kNbWindow);
 }
 
-// test knob (MPX_TEST_SKIP_PUSH=k): the k-th push of every call (1-based)
-// moves no payload bytes but is still signalled, so a correct receiver's
-// check must fail; read on every call
-int skip_push_knob() {
-    const char* v = getenv("MPX_TEST_SKIP_PUSH");
-    return v ? atoi(v) : 0;
-}
-
-// test knob (MPX_TEST_LAG_WG="rank:wg:us"): in non-blocking check mode,
-// workgroup wg of `rank` (wg < 0 counts from the last) stalls `us`
-// microseconds before it checks the call's last receive (in pull mode: before
-// it loads the call's last payload from the peer's tx), so that rank's call
-// ends long after its peer's; read per call
-void lag_knob(int my_rank, int* wg, u64* ticks) {
-    *wg = 0;
-    *ticks = 0;
-    const char* v = getenv("MPX_TEST_LAG_WG");
-    int r = -1, w = 0;
-    long long us = 0;
-    if (v && sscanf(v, "%d:%d:%lld", &r, &w, &us) == 3 && r == my_rank && us > 0) {
-        *wg = w;
-        *ticks = (u64)us * 100ull;   // s_memrealtime: 100 MHz
+// Fault injection for the tests' negative controls, all in ONE variable:
+//   MPX_TEST="skip_push=k,lag_wg=rank:wg:us,no_posted,no_pull_wait"
+//   skip_push=k     the k-th push of every call (1-based) moves no payload
+//                   bytes but is still signalled: a correct receiver's check
+//                   must fail
+//   lag_wg=r:w:us   in non-blocking check mode, workgroup w of rank r (w < 0
+//                   counts from the last) stalls `us` before it checks the
+//                   call's last receive (pull mode: before it loads the call's
+//                   last payload), so that rank's call ends long after its peer's
+//   no_posted       no receive-posted handshake (round 2's behaviour): the
+//                   negative control of tests/test_gpu_ordering.py
+//   no_pull_wait    pull mode: a sending side returns without waiting for the
+//                   peer's loads of its tx (the buffer-reuse negative control)
+// Whether the variable exists is read ONCE per process: a process that
+// starts without it (bench.py, mpx_perf) never looks again, and none of the
+// knobs can reach it.  The tests set it (empty) before their first call
+// (tests/conftest.py) and change its value between calls.
+struct TestKnobs {
+    int skip_push = 0;
+    int lag_rank = -1, lag_wg = 0;
+    long long lag_us = 0;
+    bool no_posted = false, no_pull_wait = false;
+};
+TestKnobs test_knobs() {
+    static const bool gate = getenv("MPX_TEST") != nullptr;
+    TestKnobs k;
+    if (!gate) return k;
+    const char* v = getenv("MPX_TEST");
+    if (!v) return k;
+    std::string all(v);
+    size_t pos = 0;
+    while (pos <= all.size()) {
+        size_t end = all.find(',', pos);
+        if (end == std::string::npos) end = all.size();
+        const std::string item = all.substr(pos, end - pos);
+        if (!item.compare(0, 10, "skip_push=")) k.skip_push = atoi(item.c_str() + 10);
+        else if (!item.compare(0, 7, "lag_wg=")) {
+            if (sscanf(item.c_str() + 7, "%d:%d:%lld", &k.lag_rank, &k.lag_wg, &k.lag_us) != 3) k.lag_rank = -1;
+        } else if (item == "no_posted") k.no_posted = true;
+        else if (item == "no_pull_wait") k.no_pull_wait = true;
+        pos = end + 1;
     }
-}
-
-// test knob (MPX_TEST_NO_POSTED=1): no receive-posted handshake (the sender
-// pushes call k+1 as soon as its own state allows, the round-2 behaviour);
-// the negative control of tests/test_gpu_ordering.py; read per call
-bool no_posted_knob() {
-    const char* v = getenv("MPX_TEST_NO_POSTED");
-    return v && atoi(v) != 0;
-}
-
-// test knob (MPX_TEST_NO_PULL_WAIT=1): in pull mode a sending side's call
-// returns without waiting for the peer's loads of its tx; the negative
-// control of the pull-mode buffer-reuse test (tests/test_gpu_pull.py)
-bool no_pull_wait_knob() {
-    const char* v = getenv("MPX_TEST_NO_PULL_WAIT");
-    return v && atoi(v) != 0;
-}
-
-bool plain_streams() {
-    const char* kind = getenv("MPX_STREAM");
-    return kind && !strcmp(kind, "plain");
+    return k;
 }
 
 // A rank's stream must own its hardware queue.  The two halves of a pair
@@ -374,7 +383,6 @@ bool plain_streams() {
 // queues, the second kernel waits behind the first and both time out.  A
 // stream created with a CU mask is never placed on a shared queue, so every
 // rank stream is created with a mask that enables all CUs.
-// MPX_STREAM=plain falls back to an ordinary non-blocking stream.
 //
 // Teardown rule (gfx950 / ROCm 7.2, isolated with tools/stream_teardown.hip,
 // profiles/r02_stream_teardown.txt): a CU-masked stream owns a dedicated HSA
@@ -393,13 +401,11 @@ bool plain_streams() {
 // process-lifetime objects, like the runtime's own queues: mpx_finalize
 // drains them (callback_fence), frees every allocation of the context, and
 // returns them to a per-device pool that later contexts reuse.  At exit they
-// are left to the runtime's teardown (destroy_stream_pool below): every
-// allocation their kernels touched is freed by then — the safe order.  A HIP
-// call from a library destructor after a profiler's exit handler ends in
-// SIGSEGV in __cxa_finalize (profiles/r02_prof_n2_exit.txt), so the exit
-// handler that can destroy them (MPX_POOL_EXIT A/B modes) is registered with
-// atexit() when the first rank stream is created, after the tool's, and runs
-// before it.
+// are left to the runtime's teardown: every allocation their kernels touched
+// is freed by then — the safe order (profiles/r03_exit_order_ab.txt: 4 of 4
+// clean exits in processes mode, where destroying them in an exit handler
+// after callback_fence gave 2 of 4).  Round 3's exit-handler A/B modes
+// (MPX_POOL_EXIT) are gone.
 struct StreamPool {
     std::mutex mu;
     std::map<int, std::vector<hipStream_t>> idle;    // per device
@@ -410,8 +416,6 @@ StreamPool& pool() {
     static StreamPool* p = new StreamPool;   // never destroyed: no static-destructor ordering
     return *p;
 }
-
-void destroy_stream_pool();
 
 void fence_cb(void* p) { static_cast<std::atomic<int>*>(p)->fetch_add(1, std::memory_order_release); }
 
@@ -468,19 +472,11 @@ void callback_fence(const std::vector<std::pair<int, hipStream_t>>& ss) {
 // — destroying a CU-masked stream mid-process is unsafe on this runtime
 // whatever ordering precedes it, so the pool is the design, not a default.
 void release_rank_stream(int dev, hipStream_t s) {
-    if (plain_streams()) {
-        (void)hipStreamDestroy(s);
-        return;
-    }
     std::lock_guard<std::mutex> lk(pool().mu);
     pool().idle[dev].push_back(s);
 }
 
 int create_rank_stream(int dev, hipStream_t* s) {
-    if (plain_streams()) {
-        HIPCK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-        return MPX_OK;
-    }
     {
         std::lock_guard<std::mutex> lk(pool().mu);
         auto& v = pool().idle[dev];
@@ -495,88 +491,14 @@ int create_rank_stream(int dev, hipStream_t* s) {
     const int words = (prop.multiProcessorCount + 31) / 32;
     std::vector<uint32_t> mask((size_t)words, 0xffffffffu);
     HIPCK(hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask.data()));
-    static std::once_flag registered;
-    std::call_once(registered, [] { atexit(destroy_stream_pool); });
     std::lock_guard<std::mutex> lk(pool().mu);
     pool().all.emplace_back(dev, *s);
     return MPX_OK;
 }
 
-// exit handler (registered at the first rank stream, see above).
-// By default the pooled rank streams are NOT destroyed: every context has
-// been finalized by then (each drained its streams through callback_fence
-// and freed all it allocated — the safe order), and the runtime's own exit
-// teardown releases the streams and their queues.  Measured (round 3):
-//  * left to the runtime: mpx_perf in processes mode (two processes on GPU
-//    0, IPC-mapped) 4 of 4 clean exits; exit 0 under rocprofv3 for bench.py
-//    and mpx_perf (profiles/r03_exit_order_ab.txt) — round 1's SIGSEGV in
-//    __cxa_finalize came from streams leaked with memory still allocated;
-//  * destroyed here after callback_fence: 2 of 4 clean in processes mode —
-//    the event thread stalls inside a completion callback that no fence of
-//    ours orders (it is not one of our streams' commands; a device-wide
-//    synchronize before the destroy made it 0 of 4);
-//  * destroyed 50 ms after the drain (round 2): 4 of 4, but only time orders it.
-// MPX_POOL_EXIT=destroy | devsync | sleep selects those orders (A/B).
-void destroy_stream_pool() {
-    StreamPool& p = pool();
-    std::lock_guard<std::mutex> lk(p.mu);
-    // A context still alive at exit owns memory its streams' kernels touched
-    // (see the teardown rule above); libmpx's own hosts never get here on a
-    // failure: MPX_CHECK flushes stdio and _exits (host/mpx_perf.c,
-    // integration/mpx_binding.c).
-    const char* mode = getenv("MPX_POOL_EXIT");
-    // Under rocprofv3 --pmc (it sets ROCPROF_COUNTERS) the runtime's own
-    // teardown of streams left to it runs after the profiler's tool has
-    // finalized and segfaults in __cxa_finalize, after the counters were
-    // written (round 3, tools/gpu_pmc_pull.sh's first pass; --kernel-trace
-    // runs exit cleanly).  There the default is round 2's order: drain,
-    // 50 ms, destroy here — this handler runs before the tool's.
-    if ((!mode || !*mode) && getenv("ROCPROF_COUNTERS")) mode = "sleep";
-    if (!mode || !*mode || !strcmp(mode, "keep") || p.live_contexts != 0 || p.all.empty()) return;
-    if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] exit: destroying %zu pooled rank streams\n", p.all.size());
-    int prev = -1;
-    (void)hipGetDevice(&prev);
-    if (!strcmp(mode, "sleep")) {
-        for (auto& ds : p.all) {
-            (void)hipSetDevice(ds.first);
-            (void)hipStreamSynchronize(ds.second);
-        }
-        usleep(50000);
-    } else {
-        callback_fence(p.all);
-        if (!strcmp(mode, "devsync")) {
-            for (auto& ds : p.all) {
-                (void)hipSetDevice(ds.first);
-                (void)hipDeviceSynchronize();
-            }
-            callback_fence(p.all);
-        }
-    }
-    for (auto& ds : p.all) {
-        (void)hipSetDevice(ds.first);
-        (void)hipStreamDestroy(ds.second);
-    }
-    if (prev >= 0) (void)hipSetDevice(prev);
-    p.all.clear();
-    p.idle.clear();
-    if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] exit: rank streams destroyed\n");
-}
-
 bool same_device(const Rank& a, const Rank& b) {
     if (a.local && b.local) return a.dev == b.dev;
     return a.bus_id[0] && strcmp(a.bus_id, b.bus_id) == 0;
-}
-
-// LL protocol A/B knob (DESIGN.md "LL"): MPX_LL_FLAGS=4 re-reads tx at every
-// LL send instead of holding the payload in registers.  The 8-B granule and
-// sentinel-poll variants of the first LL A/B (profiles/r01_ll_ab.jsonl) lost
-// and were removed.
-int ll_flags() {
-    static const int f = [] {
-        const char* v = getenv("MPX_LL_FLAGS");
-        return v ? atoi(v) : 0;
-    }();
-    return f;
 }
 
 // Non-blocking mode: a push is published (kernel engine: drained + flag;
@@ -611,11 +533,15 @@ u64 timeout_ticks(const mpx_xfer_opts* o) {
 // ---------------------------------------------------------------------------
 // engine: kernel
 // ---------------------------------------------------------------------------
+int ensure_peer_tx_locked(mpx_ctx* ctx, Rank& peer, int peer_rank);
 // Pull mode loads from the peer's tx: an imported rank's tx is mapped here on
 // first use (under the context lock: both halves of a pair, or several local
 // ranks, may get here at once), on the device imports are opened on.
 int ensure_peer_tx(mpx_ctx* ctx, Rank& peer, int peer_rank) {
     std::lock_guard<std::mutex> lk(ctx->mu);
+    return ensure_peer_tx_locked(ctx, peer, peer_rank);
+}
+int ensure_peer_tx_locked(mpx_ctx* ctx, Rank& peer, int peer_rank) {
     if (peer.tx) return MPX_OK;
     if (!peer.imported || !peer.tx_handle_valid)
         return fail(MPX_ERR_STATE, "pull mode: rank %d's tx is not known here", peer_rank);
@@ -632,13 +558,60 @@ int ensure_peer_tx(mpx_ctx* ctx, Rank& peer, int peer_rank) {
     return MPX_OK;
 }
 
+// How a kernel-engine call waits for its kernel (MPX_SYNC, read once):
+//   query (default) — spin on the host-mapped completion word the kernel's
+//           last workgroup stores (Status.done), then on hipEventQuery of the
+//           end event: the call returns once the kernel has retired (its
+//           writes visible to every later command), with no interrupt on
+//           the way;
+//   event — hipEventSynchronize (round 3's form: the runtime's blocking
+//           wait, woken by an interrupt once its short active spin expires).
+// run-hbv3's 456131 B x 10 calls carried ~21 us of fixed
+// cost each; mpx_last_phases reports where a call's time goes.
+enum SyncMode { kSyncQuery = 0, kSyncEvent = 1 };
+int sync_mode() {
+    static const int m = [] {
+        const char* v = getenv("MPX_SYNC");
+        return (v && !strcmp(v, "event")) ? kSyncEvent : kSyncQuery;
+    }();
+    return m;
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// Wait until the call's kernel (end event ev1) has completed; *t_done = the
+// host time the completion word was first seen (0 in event mode).
+int wait_kernel(Rank& me, u64 token, double* t_done) {
+    *t_done = 0;
+    if (sync_mode() == kSyncEvent) {
+        HIPCK(hipEventSynchronize(me.ev1));
+        return MPX_OK;
+    }
+    // Before the word arrives the end event is polled only every 50 us (a
+    // kernel that could not launch never stores it); after, back to back.
+    double next_query = now_s() + 50e-6;
+    for (;;) {
+        if (*t_done == 0 && __atomic_load_n(&me.status->done, __ATOMIC_ACQUIRE) == token) *t_done = now_s();
+        if (*t_done != 0 || now_s() >= next_query) {
+            const hipError_t q = hipEventQuery(me.ev1);
+            if (q == hipSuccess) {
+                if (*t_done == 0) *t_done = now_s();
+                return MPX_OK;
+            }
+            if (q != hipErrorNotReady) HIPCK(q);
+            next_query = now_s() + 50e-6;
+        }
+        cpu_relax();
+    }
+}
+
 int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters,
                long long len, const mpx_xfer_opts* o, mpx_timing* t) {
+    const double t_call = now_s();
     XferArgs a{};
     a.tx = me.tx;
     a.rx = me.rx;
     a.peer_rx = peer.rx;
-    a.peer_tx = peer.tx;
     a.my_mb = me.mb;
     a.peer_mb = peer.mb;
     a.status = me.status;
@@ -673,20 +646,18 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
         return v && atoi(v) != 0;
     }();
     a.stream = ((o && (o->flags & MPX_XFER_STREAM)) || env_stream) ? 1 : 0;
-    a.ll_flags = ll_flags();
     a.nb_publish = nb_publish();
     a.ll_max = ll_max_bytes(same_device(me, peer));
     if (const char* v = getenv("MPX_LL_MAX")) a.ll_max = atoi(v) < kLLMaxBytes ? atoi(v) : kLLMaxBytes;
-    a.ring = me.ring;
-    a.peer_ring = peer.ring;
     a.cnt = me.cnt;
-    a.slots = link_slots(me, peer, len);
-    a.skip_push = skip_push_knob();
-    a.no_pull_wait = no_pull_wait_knob() ? 1 : 0;
-    lag_knob(my_rank, &a.lag_wg, &a.lag_ticks);
+    const TestKnobs knobs = test_knobs();
+    a.skip_push = knobs.skip_push;
+    a.no_pull_wait = knobs.no_pull_wait ? 1 : 0;
+    if (knobs.lag_rank == my_rank && knobs.lag_us > 0) {
+        a.lag_wg = knobs.lag_wg;
+        a.lag_ticks = (u64)knobs.lag_us * 100ull;   // s_memrealtime: 100 MHz
+    }
     if (a.lag_wg < 0) a.lag_wg += a.nwg;   // -1: the last pushing workgroup
-    if (!pull_requested(o) && a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!me.ring || !peer.ring))
-        return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
 
     const bool ll = mode != MPX_MODE_NONBLOCKING && len <= a.ll_max;
     const bool pushes_len = mode != MPX_MODE_UNIDIR || group == 1;
@@ -695,19 +666,23 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     // LL messages stay pushes.  A receiving side runs nwg workgroups (one
     // chunk each), unidir group 1 one (it only publishes and takes acks).
     a.pull = (!ll && pull_requested(o)) ? 1 : 0;
-    if (a.pull && !peer.tx) {
-        TRY(ensure_peer_tx(ctx, peer, peer_rank));
+    {
+        // fields another rank's thread may set at the same time (a lazily
+        // mapped tx, a lazily allocated ring) are read under the context lock
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (a.pull) TRY(ensure_peer_tx_locked(ctx, peer, peer_rank));
         a.peer_tx = peer.tx;
+        a.ring = me.ring;
+        a.peer_ring = peer.ring;
+        a.slots = link_slots(me, peer, len);
     }
+    if (!a.pull && a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!a.ring || !a.peer_ring))
+        return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
     const int grid = a.pull ? (recvs_len ? a.nwg : 1)
                             : (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;
     // bulk pushes read tx from LDS when one workgroup's chunk fits
-    // (kStageMaxBytes); MPX_STAGE=0 turns it off (A/B)
-    static const bool stage_on = [] {
-        const char* v = getenv("MPX_STAGE");
-        return !(v && atoi(v) == 0);
-    }();
-    if (stage_on && !ll && !a.pull && pushes_len && len > 0) {
+    // (kStageMaxBytes); the call's MPX_XFER_NOSTAGE flag reads it from HBM
+    if (!(o && (o->flags & MPX_XFER_NOSTAGE)) && !ll && !a.pull && pushes_len && len > 0) {
         static const long long lds_cap = [] {
             int dev = 0, per_block = 0;
             (void)hipGetDevice(&dev);
@@ -719,7 +694,8 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
         if (chunk <= kStageMaxBytes && chunk <= lds_cap) a.stage = (int)chunk;
     }
 
-    HIPCK(hipMemsetAsync(me.scratch, 0, 4 * sizeof(u64), me.stream));
+    // (scratch words [0..3] are zero: the previous call's last workgroup
+    // reset them — no memset on the stream ahead of the kernel)
     if (a.check) {
         HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
         if (mode == MPX_MODE_NONBLOCKING) HIPCK(hipMemsetAsync(me.cnt, 0, (size_t)iters * sizeof(u64), me.stream));
@@ -728,17 +704,21 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     me.status->where = 0;
     me.status->recv_done = 0;
     me.status->recv_digest = 0;
+    me.status->t_entry = me.status->t_posted = me.status->t_exit = 0;
+    a.done_token = ++me.token;
 
     // a call that moves nothing (iters = 0) posts nothing new: the count
     // stays equal on both sides even if only one side makes such a call
     a.call = iters > 0 ? ++me.calls[peer_rank] : me.calls[peer_rank];
-    if (no_posted_knob()) a.call = 0;   // every wait for posted >= 0 holds at once
+    if (knobs.no_posted) a.call = 0;   // every wait for posted >= 0 holds at once
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
     HIPCK(launch_xfer(a, grid, me.stream));
     HIPCK(hipEventRecord(me.ev1, me.stream));
-    HIPCK(hipEventSynchronize(me.ev1));
-    t->wall_s = now_s() - t0;
+    double t_done = 0;
+    TRY(wait_kernel(me, a.done_token, &t_done));
+    const double t_end = now_s();
+    t->wall_s = t_end - t0;
     float ms = 0;
     HIPCK(hipEventElapsedTime(&ms, me.ev0, me.ev1));
     t->device_s = ms * 1e-3;
@@ -747,6 +727,21 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     t->protocol = ll ? kProtoLL : a.pull ? kProtoPull : kProtoBulk;
     t->recv_done = __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE);
     t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
+    // phases (mpx_last_phases): the kernel's own clock splits its span; the
+    // host's clock brackets it (launch before, completion after)
+    const u64 te = __atomic_load_n(&me.status->t_entry, __ATOMIC_ACQUIRE);
+    const u64 tp = __atomic_load_n(&me.status->t_posted, __ATOMIC_ACQUIRE);
+    const u64 tx = __atomic_load_n(&me.status->t_exit, __ATOMIC_ACQUIRE);
+    mpx_phases& ph = me.phases;
+    ph = mpx_phases{};
+    ph.wall_s = t->wall_s;
+    ph.host_prep_s = t0 - t_call;
+    ph.kernel_s = (te && tx >= te) ? (double)(tx - te) * 1e-8 : 0;
+    ph.posted_wait_s = (te && tp >= te) ? (double)(tp - te) * 1e-8 : 0;
+    if (t_done > 0 && ph.kernel_s > 0) {
+        ph.launch_to_start_s = (t_done - t0) - ph.kernel_s;
+        ph.done_to_return_s = t_end - t_done;
+    }
     const unsigned err = __atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE);
     if (err) {
         me.broken = true;
@@ -1045,7 +1040,7 @@ int sdma_chunk_graph(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode,
 int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters, long long len,
              const mpx_xfer_opts* o, mpx_timing* t, bool pull) {
     SdmaOps op{me, peer, my_rank, peer_rank, timeout_ticks(o)};
-    op.skip = skip_push_knob();
+    op.skip = test_knobs().skip_push;
     op.pull = pull;
     const int check = (o && o->check) ? 1 : 0;
     const int slots = link_slots(me, peer, len);
@@ -1072,7 +1067,7 @@ int run_sdma(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     // matched-receive order (Mailbox.posted), stream-ordered: post this
     // call's receives, and a side that pushes first waits for the peer's
     // post before its first copy into the peer's rx
-    if (iters > 0 && !no_posted_knob()) {
+    if (iters > 0 && !test_knobs().no_posted) {
         const u64 call = ++me.calls[peer_rank];
         TRY(op.signal_abs(&peer.mb->posted[my_rank], call));
         if (mode == MPX_MODE_NONBLOCKING || group == 1) TRY(op.wait_abs(&me.mb->posted[peer_rank], call));
@@ -1139,7 +1134,7 @@ int run_rccl(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
     me.status->recv_done = 0;
     me.status->recv_digest = 0;
     const size_t n = (size_t)len;
-    const int skip = skip_push_knob();
+    const int skip = test_knobs().skip_push;
     const double t0 = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
     int launches = 0, inflight = 0;
@@ -1251,6 +1246,13 @@ int mpx_link_info(int dev_a, int dev_b, int* link_type, int* hops) {
     HIPCK(hipExtGetLinkTypeAndHopCount(dev_a, dev_b, &t, &h));
     *link_type = (int)t;
     *hops = (int)h;
+    return MPX_OK;
+}
+
+int mpx_device_bus_id(int dev, char* buf, int len) {
+    if (!buf || len < 16) return fail(MPX_ERR_INVALID, "bus id buffer too small");
+    TRY(check_dev(dev));
+    HIPCK(hipDeviceGetPCIBusId(buf, len, dev));
     return MPX_OK;
 }
 
@@ -1467,11 +1469,14 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     HIPCK(hipEventCreate(&e1));
     int grid = 0;
     // All iterations in one launch where a launch per copy is dispatch-bound:
-    // k_copy_pipe above 512 KiB to 16 MiB, k_copy_steps up to 512 KiB (and up
-    // to copy_steps_max() where the pipe is off); one k_copy launch per copy
-    // above (profiles/r03_copy_pipe_ab.jsonl)
-    const bool pipe = n && iters > 1 && n > copy_pipe_min() && n <= copy_pipe_max();
-    bool steps = !pipe && n && iters > 1 && n <= copy_steps_max();
+    // k_copy_pipe above 512 KiB to 16 MiB, k_copy_steps up to 512 KiB; one
+    // k_copy launch per copy above (profiles/r03_copy_pipe_ab.jsonl, DESIGN.md
+    // §5) — or the form MPX_COPY forces (copy_choice)
+    const CopyChoice cc = copy_choice();
+    const bool multi = n && iters > 1;
+    bool pipe = multi && (cc.form == kCopyPipe ||
+                          (cc.form == kCopyAuto && n > kCopyPipeDefaultMin && n <= kCopyPipeDefaultMax));
+    const bool steps = multi && !pipe && (cc.form == kCopySteps || (cc.form == kCopyAuto && n <= kCopyPipeDefaultMin));
     bool one = pipe || steps;          // all copies in one launch
     u64* bar = ctx->dev_tmp[dev] + 16;
     float ms = 0;
@@ -1480,10 +1485,18 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
         if (one) HIPCK(hipMemsetAsync(bar, 0, 17 * 16 * sizeof(u64), s));   // top + 8 group counters + 8 release words
         t0 = now_s();
         HIPCK(hipEventRecord(e0, s));
-        if (one && pipe)
-            HIPCK(launch_copy_pipe(dst, src, n, iters, bar, s, &grid));
-        else if (one)
-            HIPCK(launch_copy_steps(dst, src, n, iters, bar, s, &grid));
+        if (one && pipe) {
+            const hipError_t e = launch_copy_pipe(dst, src, n, iters, bar, s, &grid, cc.upl, cc.hier);
+            if (e == hipErrorInvalidValue) {
+                // too large for a resident pipe grid (a forced form or shape):
+                // a launch per copy instead
+                (void)hipGetLastError();
+                one = pipe = false;
+                continue;
+            }
+            HIPCK(e);
+        } else if (one)
+            HIPCK(launch_copy_steps(dst, src, n, iters, bar, s, &grid, cc.shaped ? cc.shape : nullptr));
         else
             for (int i = 0; i < iters && n; ++i) HIPCK(launch_copy(dst, src, n, s, &grid));
         HIPCK(hipEventRecord(e1, s));
@@ -1814,6 +1827,13 @@ int mpx_xfer(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, i
     const int st = mpx_xfer_ex(ctx, mode, my_group, my_rank, peer_rank, iters, tx, rx, buff_len, nullptr, &t);
     if (sec) *sec = t.wall_s;
     return st;
+}
+
+int mpx_last_phases(mpx_ctx* ctx, int rank, mpx_phases* out) {
+    if (!ctx || !out) return fail(MPX_ERR_INVALID, "NULL argument");
+    if (rank < 0 || rank >= ctx->nranks || !ctx->r[rank].local) return fail(MPX_ERR_STATE, "rank %d is not a local rank", rank);
+    *out = ctx->r[rank].phases;
+    return MPX_OK;
 }
 
 int mpx_barrier(mpx_ctx* ctx, int nthreads) {

@@ -30,7 +30,8 @@ MODES = {"pingpong": MODE_PINGPONG, "nonblocking": MODE_NONBLOCKING, "unidir": M
 FILL_BYTE, FILL_SPLITMIX = 0, 1
 XFER_STREAM = 1
 XFER_PULL = 2
-ABI_VERSION = 5
+XFER_NOSTAGE = 4
+ABI_VERSION = 6
 PATTERN_SEED = 0x6D70695F70657266
 MAX_RANKS = 64
 RANK_DESC_BYTES = 512
@@ -69,6 +70,14 @@ class XferOpts(C.Structure):
     ]
 
 
+class Phases(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",
+                                           "done_to_return_s")]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 def pattern_key(seed: int, src: int, dst: int, it: int) -> int:
     """mpx_pattern_key (include/mpx.h)."""
     return (seed ^ (src << 56) ^ (dst << 48) ^ (it << 24)) & 0xFFFFFFFFFFFFFFFF
@@ -80,6 +89,8 @@ _SIGS = {
     "mpx_last_error": (C.c_char_p, []),
     "mpx_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "mpx_link_info": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "mpx_device_bus_id": (C.c_int, [C.c_int, C.c_char_p, C.c_int]),
+    "mpx_last_phases": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Phases)]),
     "mpx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "mpx_finalize": (C.c_int, [C.c_void_p]),
     "mpx_alloc": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]),
@@ -150,6 +161,13 @@ def link_info(dev_a: int, dev_b: int) -> dict:
     t, h = C.c_int(0), C.c_int(0)
     check(lib().mpx_link_info(dev_a, dev_b, C.byref(t), C.byref(h)), "mpx_link_info")
     return {"type": LINK_TYPES.get(t.value, t.value), "hops": h.value}
+
+
+def bus_id(dev: int) -> str:
+    """mpx_device_bus_id: the GPU's PCI bus id, "DDDD:BB:DD.F"."""
+    buf = C.create_string_buffer(64)
+    check(lib().mpx_device_bus_id(dev, buf, 64), "mpx_device_bus_id")
+    return buf.value.decode()
 
 
 @dataclass
@@ -225,8 +243,9 @@ class Context:
 
     def xfer(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, tx: Buffer, rx: Buffer,
              length: int, check_payload: bool = False, expect: int = 0, expect_ack: int = 0,
-             timeout_ms: int = 0, nwg: int = 0, stream: bool = False, pull: bool = False) -> Timing:
-        flags = (XFER_STREAM if stream else 0) | (XFER_PULL if pull else 0)
+             timeout_ms: int = 0, nwg: int = 0, stream: bool = False, pull: bool = False,
+             stage: bool = True) -> Timing:
+        flags = (XFER_STREAM if stream else 0) | (XFER_PULL if pull else 0) | (0 if stage else XFER_NOSTAGE)
         o = XferOpts(check=1 if check_payload else 0, flags=flags, expect_checksum=expect,
                      expect_ack=expect_ack, timeout_ms=timeout_ms, nwg=nwg)
         t = Timing()
@@ -243,6 +262,12 @@ class Context:
         o = XferOpts(timeout_ms=timeout_ms, flags=XFER_PULL if pull else 0)
         check(self.L.mpx_xfer_prepare(self.h, mode, group, my_rank, peer_rank, iters, length, C.byref(o)),
               "mpx_xfer_prepare")
+
+    def phases(self, rank: int) -> dict:
+        """mpx_last_phases: where rank's last kernel-engine call spent its time"""
+        p = Phases()
+        check(self.L.mpx_last_phases(self.h, rank, C.byref(p)), "mpx_last_phases")
+        return p.as_dict()
 
     def rccl_init_all(self) -> None:
         check(self.L.mpx_rccl_init_all(self.h), "mpx_rccl_init_all")

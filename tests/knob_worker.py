@@ -12,6 +12,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import mpx  # noqa: E402
 
 CAP = (1 << 20) + 9
+STAGE = os.environ.get("WORKER_NOSTAGE") != "1"   # the call flag MPX_XFER_NOSTAGE (bulk pushes read tx from HBM)
 for engine in ("kernel", "sdma", "kernel-pull", "sdma-pull"):
     pull = engine.endswith("-pull")
     with mpx.Context(2, engine[:-len("-pull")] if pull else engine) as c:
@@ -30,7 +31,7 @@ for engine in ("kernel", "sdma", "kernel-pull", "sdma-pull"):
                 def side(r):
                     try:
                         t = c.xfer(mode, 1 - r, r, 1 - r, iters, bufs[r][0], bufs[r][1], n, check_payload=check,
-                                   expect=exp[r][0], expect_ack=exp[r][1], timeout_ms=10000, pull=pull)
+                                   expect=exp[r][0], expect_ack=exp[r][1], timeout_ms=10000, pull=pull, stage=STAGE)
                         assert t.check_failures == 0
                     except Exception as e:  # noqa: BLE001
                         errs.append(f"{engine} mode {mode} n {n} rank {r}: {e}")

@@ -13,7 +13,7 @@ rank 1 between two calls and changing its payload (pattern A, then B):
   must still hold call 1's last payload (pattern A), and after call 2 the
   new one (pattern B).
 * lag: the non-blocking loop in check mode; one of rank 1's workgroups stalls
-  (MPX_TEST_LAG_WG) before it checks call 1's last receive, and call 2 changes
+  (MPX_TEST lag_wg=...) before it checks call 1's last receive, and call 2 changes
   the length and the push width, so its chunks and receive slots cover bytes
   the stalled workgroup still owns under call 1's layout.  Every payload of
   both calls must pass its checksum.
@@ -42,8 +42,10 @@ RACE_DELAY_S = 0.3
 SIZES = (1, 1024, 4097, 65536 + 13, 262144 + 13, LAG_N1, LAG_N2)
 
 
-def lag_env() -> dict:
-    return {"MPX_TEST_LAG_WG": f"1:{LAG_WG}:{LAG_US}"}
+def lag_env(extra: str = "") -> dict:
+    """libmpx's fault injection for the lag scenario (MPX_TEST lag_wg=...),
+    plus `extra` knobs (e.g. "no_posted")"""
+    return {"MPX_TEST": ",".join(x for x in (f"lag_wg=1:{LAG_WG}:{LAG_US}", extra) if x)}
 
 
 def key(rank: int, peer: int, it: int) -> int:

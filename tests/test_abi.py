@@ -29,8 +29,9 @@ def test_every_header_symbol_is_exported():
 def test_version_and_strerror():
     L = mpx.lib()
     # 2: recv_done / recv_digest; 3: 64 ranks per context; 4: receive-posted mailbox word;
-    # 5: pull mode (MPX_XFER_PULL, tx in the rank descriptor)
-    assert L.mpx_version() == 5
+    # 5: pull mode (MPX_XFER_PULL, tx in the rank descriptor); 6: mpx_last_phases,
+    # mpx_device_bus_id, MPX_XFER_NOSTAGE, kernel-cleared scratch words
+    assert L.mpx_version() == 6
     texts = {L.mpx_strerror(i).decode() for i in range(9)}
     assert len(texts) == 9
     assert L.mpx_strerror(12345) == b"unknown mpx status"

@@ -47,7 +47,7 @@ def test_fill_and_checksum_match_oracle(ctx, n, pattern):
                                (1 << 20) + 3, (2 << 20) + 16, (8 << 20) + 1])
 def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
     """k_copy_steps (all copies in one launch, grid barrier between steps),
-    forced at every size (MPX_COPY_STEPS_MAX): the grid classes of its
+    forced at every size (MPX_COPY=steps): the grid classes of its
     defaults (1024-lane workgroups, one unit per lane: one workgroup up to
     16 KiB, <= 64 workgroups up to 1 MiB; 64 256-lane workgroups with 8
     units per lane above, in load batches) on both sides of each class
@@ -56,8 +56,7 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
     counters, drain, units per lane, 256 / 512 / 1024 lanes, every working
     workgroup on one XCD) at 1 MiB + 3:
     output against the oracle's pattern, nothing written past the end."""
-    monkeypatch.setenv("MPX_COPY_STEPS_MAX", str(16 << 20))
-    monkeypatch.setenv("MPX_COPY_PIPE_MAX", "0")
+    monkeypatch.setenv("MPX_COPY", "steps")
     key = mpx.pattern_key(mpx.PATTERN_SEED, 1, 1, n & 0xFFFF)
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
     try:
@@ -68,7 +67,7 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
                              if n == (1 << 20) + 3 else [])
         for v in variants:
             if v:
-                monkeypatch.setenv("MPX_COPY_STEPS", v)
+                monkeypatch.setenv("MPX_COPY", "steps:" + v)
             ctx.fill(dst, n + 64, mpx.FILL_BYTE, 0xEE)
             t = ctx.copy(0, dst, src, n, iters)
             # one copy is one plain k_copy launch; more run as k_copy_steps
@@ -88,15 +87,12 @@ def test_copy_steps_every_size_class(ctx, monkeypatch, n, iters):
 def test_copy_pipe_every_size_class(ctx, monkeypatch, n, iters, upl):
     """k_copy_pipe (all copies in one launch; copy s+1's loads in flight
     across copy s's grid barrier; a dedicated barrier wave), forced at every
-    size (MPX_COPY_PIPE_MAX) and units-per-lane choice (MPX_COPY_PIPE_UPL; 0 =
+    size (MPX_COPY=pipe) and units-per-lane choice (MPX_COPY=pipe:<upl>; 0 =
     the default 4, widened until the grid stays resident): odd and even copy
     counts (the loop is unrolled by two), a tail below 16 B with and without
     a body, a grid of one: output against the oracle's pattern, nothing
     written past the end."""
-    monkeypatch.setenv("MPX_COPY_PIPE_MAX", str(32 << 20))
-    monkeypatch.setenv("MPX_COPY_PIPE_MIN", "0")
-    if upl:
-        monkeypatch.setenv("MPX_COPY_PIPE_UPL", str(upl))
+    monkeypatch.setenv("MPX_COPY", f"pipe:{upl}")
     key = mpx.pattern_key(mpx.PATTERN_SEED, 2, 2, (n + upl) & 0xFFFF)
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
     try:
@@ -122,7 +118,7 @@ def test_copy_steps_grid_rule(ctx, monkeypatch, n, grid):
     128 KiB, 1024-lane ones on one XCD to 512 KiB; up to 64 1024-lane
     workgroups over every XCD to 1 MiB (above 512 KiB only with the pipe off,
     as here).  timing.nwg = working workgroups."""
-    monkeypatch.setenv("MPX_COPY_PIPE_MAX", "0")
+    monkeypatch.setenv("MPX_COPY", "steps")
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n)
     try:
         ctx.fill(src, n, mpx.FILL_BYTE, 0x5C)
@@ -163,10 +159,7 @@ def test_copy_pipe_barrier_forms(ctx, monkeypatch, n, upl, iters, hier):
     + release words) at grids of 1, 5, 4 (fewer workgroups than groups), 65,
     129 (groups of unequal size), 128 and 144 workgroups, odd and even copy
     counts: output against the oracle, nothing written past the end."""
-    monkeypatch.setenv("MPX_COPY_PIPE_MAX", str(32 << 20))
-    monkeypatch.setenv("MPX_COPY_PIPE_MIN", "0")
-    monkeypatch.setenv("MPX_COPY_PIPE_UPL", str(upl))
-    monkeypatch.setenv("MPX_COPY_PIPE_HIER", hier)
+    monkeypatch.setenv("MPX_COPY", f"pipe:{upl}:{hier}")
     key = mpx.pattern_key(mpx.PATTERN_SEED, 3, 3, (n + iters) & 0xFFFF)
     src, dst = ctx.alloc(0, n), ctx.alloc(0, n + 64)
     try:
@@ -381,11 +374,11 @@ def test_nonblocking_every_payload_seeded(engine, n):
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("skip", [1, 7, 256])
 def test_lost_payload_fails_the_check(monkeypatch, engine, mode, skip):
-    """Test knob MPX_TEST_SKIP_PUSH=k: the k-th push of each call moves no
+    """Test knob MPX_TEST=skip_push=k: the k-th push of each call moves no
     payload bytes but is still signalled.  Check mode must then report the
     receive that never got its payload (a checker that only looked at the
     final rx, or took receive counts from elsewhere, would pass)."""
-    monkeypatch.setenv("MPX_TEST_SKIP_PUSH", str(skip))
+    monkeypatch.setenv("MPX_TEST", f"skip_push={skip}")
     n = 65541 if skip != 7 else 1000   # 1000 B: the LL protocol for ping-pong / unidir
     P = Pairs(engine, 1, n, fill="seeded")
     try:
@@ -509,8 +502,8 @@ PROTO_LL = 0
 
 
 @pytest.mark.parametrize("knobs", [
-    {"MPX_STAGE": "0", "MPX_NB_PUBLISH": "1", "MPX_SDMA_GRAPH": "0"},
-    {"MPX_PUSH_STREAM": "1", "MPX_LL_FLAGS": "4", "MPX_NB_PUBLISH": "256", "MPX_PUSH_WG": "7"},
+    {"WORKER_NOSTAGE": "1", "MPX_NB_PUBLISH": "1", "MPX_SDMA_GRAPH": "0", "MPX_SYNC": "event"},
+    {"MPX_PUSH_STREAM": "1", "MPX_NB_PUBLISH": "256", "MPX_PUSH_WG": "7"},
     {"MPX_LL_MAX": "8192", "MPX_NB_PUBLISH": "2", "MPX_CHECK_RING_BYTES": "0"},   # one receive slot per link
 ])
 def test_env_knob_variants(knobs):
@@ -691,7 +684,7 @@ def test_self_pair_receive_digest_matches_reference(name, engine):
 
 @pytest.mark.parametrize("engine", ["kernel", "sdma", "rccl"])
 def test_self_pair_lost_payload_fails(monkeypatch, engine):
-    monkeypatch.setenv("MPX_TEST_SKIP_PUSH", "3")
+    monkeypatch.setenv("MPX_TEST", "skip_push=3")
     c, tx, rx = _self_rank(engine, 65541)
     try:
         with pytest.raises(mpx.MpxError) as e:

@@ -6,7 +6,7 @@ posted receive (/root/reference/mpi_perf.c:75,79,100,104,137,141).  Rank 0
 races ahead of rank 1 between two calls with a new payload:
 
 * test_*_lagging_workgroup_*: the non-blocking loop in check mode, one of rank
-  1's workgroups late to check call 1's last receive (MPX_TEST_LAG_WG), call 2
+  1's workgroups late to check call 1's last receive (MPX_TEST lag_wg=...), call 2
   with another length and push width.  Before the receive-posted handshake,
   rank 0's call 2 pushed into rank 1's rx while that workgroup still checked
   it: GPUTEST_r02's "1 of 300 received payloads failed the checksum".
@@ -132,12 +132,11 @@ def test_pull_lagging_receiver_keeps_the_senders_tx_processes(tmp_path):
 
 
 def test_pull_lagging_receiver_fails_without_the_wait(monkeypatch):
-    """Negative control: MPX_TEST_NO_PULL_WAIT=1 lets rank 0's call return
+    """Negative control: MPX_TEST=no_pull_wait lets rank 0's call return
     before rank 1's stalled workgroup loaded its chunk; rank 0's new tx then
     lands in call 1's last payload and rank 1's check reports it."""
-    for k, v in O.lag_env().items():
+    for k, v in O.lag_env("no_pull_wait").items():
         monkeypatch.setenv(k, v)
-    monkeypatch.setenv("MPX_TEST_NO_PULL_WAIT", "1")
     out = run_threads(lambda c, r, tx, rx, s: O.lag(c, r, tx, rx, s, pull=True))
     assert not out[1]["call1"]["ok"] and "failed the checksum" in out[1]["call1"]["error"], out
 
@@ -171,20 +170,19 @@ def test_rx_read_between_calls_processes(tmp_path, engine, mode):
 
 
 # ---- negative controls: the same scenarios without the handshake ----------
-# MPX_TEST_NO_POSTED=1 restores round 2's behaviour (a sender pushes call k+1
+# MPX_TEST=no_posted restores round 2's behaviour (a sender pushes call k+1
 # as soon as its own sequence and credit state allows).  Both scenarios must
 # then fail, which shows they detect the race they are there for.
 
 def test_lagging_workgroup_fails_without_the_handshake(monkeypatch):
-    for k, v in O.lag_env().items():
+    for k, v in O.lag_env("no_posted").items():
         monkeypatch.setenv(k, v)
-    monkeypatch.setenv("MPX_TEST_NO_POSTED", "1")
     out = run_threads(O.lag)
     assert not out[1]["call1"]["ok"] and "failed the checksum" in out[1]["call1"]["error"], out
 
 
 def test_rx_read_between_calls_fails_without_the_handshake(monkeypatch):
-    monkeypatch.setenv("MPX_TEST_NO_POSTED", "1")
+    monkeypatch.setenv("MPX_TEST", "no_posted")
     n, iters = RACE_CASES[0]
     out = run_threads(lambda c, r, tx, rx, s: O.race(c, r, tx, rx, s, mpx.MODE_PINGPONG, False, n, iters))
     assert not out[1]["rx_between_is_call1"], out

@@ -163,10 +163,10 @@ def test_pull_nonblocking_every_payload_seeded(n, engine):
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("skip", [1, 7, 256])
 def test_pull_lost_payload_fails_the_check(monkeypatch, mode, skip, engine):
-    """MPX_TEST_SKIP_PUSH=k in pull mode: the k-th receive of each call loads
+    """MPX_TEST=skip_push=k in pull mode: the k-th receive of each call loads
     nothing (its ready word and credit still go), so check mode must report
     the receive whose bytes never came."""
-    monkeypatch.setenv("MPX_TEST_SKIP_PUSH", str(skip))
+    monkeypatch.setenv("MPX_TEST", f"skip_push={skip}")
     P = Pairs(engine, 1, 65541, fill="seeded")
     try:
         out, errs = P.run(mode, 65541, 300, pull=True)

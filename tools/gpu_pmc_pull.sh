@@ -13,7 +13,6 @@ export TMPDIR=/tmp
 # runtime tears the streams down after the tool finalized.  Round 2's exit
 # order (drain, 50 ms, destroy in libmpx's exit handler, which runs before
 # the tool's) keeps these runs clean.
-export MPX_POOL_EXIT=sleep
 O=gpurun_out/pmc_pull
 mkdir -p $O
 run_self() {   # name variant B iters [env]
@@ -40,7 +39,7 @@ run_pair() {   # name mode B iters check pull
 }
 for b in 4096 456131 4194304 67108864; do
     run_self nbpull_$b nbpull $b 256 || exit 1
-    run_self nbpush_$b nb_hbm $b 256 MPX_STAGE=0 || exit 1
+    run_self nbpush_$b nb_hbm $b 256 || exit 1
 done
 run_self nbpullcheck_4194304 nbpullcheck 4194304 256 || exit 1
 run_pair uni_pull_4194304 unidir 4194304 500 0 pull || exit 1

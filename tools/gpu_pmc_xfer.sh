@@ -32,7 +32,7 @@ run_pair() {   # name mode B iters check
 }
 for b in 4096 456131 4194304; do
     run_self nb_$b nb $b 512 || exit 1
-    run_self nbhbm_$b nb_hbm $b 512 MPX_STAGE=0 || exit 1
+    run_self nbhbm_$b nb_hbm $b 512 || exit 1
     run_self nbcheck_$b nbcheck $b 512 || exit 1
 done
 run_pair pp_ll_8 pingpong 8 4000 0 || exit 1

@@ -30,7 +30,6 @@ export TMPDIR=/tmp WORLD_SIZE=$N MASTER_ADDR=127.0.0.1
 # exit handler, before the profiler's): under rocprofv3 --pmc the default
 # (streams left to the runtime's teardown) segfaults in __cxa_finalize after
 # the profiler wrote its output (tools/gpu_pmc_pull.sh, round 3)
-export MPX_POOL_EXIT=sleep
 STEPS=${STEPS:-$((2 * (N - 1)))}
 run_pass() {   # pass-name, rocprofv3 options...
     local pass=$1; shift

@@ -5,8 +5,8 @@ one launch moves `iters` pushes of B bytes (DESIGN.md §7 "Counter evidence").
       one rank paired with itself on GPU 0: the non-blocking loop as ONE
       kernel (k_xfer<1,0>, or k_xfer_nbcheck with check) — nothing for the
       profiler's dispatch serialisation to deadlock.  variant: nb (bulk, LDS-
-      staged tx), nb_hbm (bulk, tx read from HBM: MPX_STAGE=0 set by the
-      caller), nbcheck (bulk + every payload checksummed and poisoned),
+      staged tx), nb_hbm (bulk, tx read from HBM: the call flag
+      MPX_XFER_NOSTAGE), nbcheck (bulk + every payload checksummed and poisoned),
       nbpull / nbpullcheck (pull mode, MPX_XFER_PULL: k_xfer_pull loads its
       own tx every iteration — whether each iteration's bytes come from
       memory or from the L2 is what FETCH_SIZE shows).
@@ -41,7 +41,8 @@ def self_pair(variant, B, iters):
         check = variant in ("nbcheck", "nbpullcheck")
         pull = variant.startswith("nbpull")
         for _ in range(3):
-            t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, B, check_payload=check, expect=want, pull=pull)
+            t = c.xfer(mpx.MODE_NONBLOCKING, 0, 0, 0, iters, tx, rx, B, check_payload=check, expect=want, pull=pull,
+                       stage=variant != "nb_hbm")
         assert c.checksum(rx, B) == want
         print(json.dumps(dict(variant=variant, bytes=B, iters=iters, nwg=t.nwg, protocol=mpx.PROTOCOLS[t.protocol],
                               us_per_push=round(t.device_s / iters * 1e6, 3), check_iters=t.check_iters)))

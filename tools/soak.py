@@ -10,7 +10,7 @@ mode every payload is checksummed on the device.
     python tools/soak.py worker <dir> <rank> <calls> <seed> <engine>   (one process of `procs`)
 
 engine: kernel (default) or sdma; both with push and pull calls.  With a
-negative-control knob set (MPX_TEST_NO_POSTED=1, MPX_TEST_NO_PULL_WAIT=1) the
+negative-control knob set (MPX_TEST=no_posted, MPX_TEST=no_pull_wait) the
 soak must report failures: that is what shows it can see the races.
 
 Prints one JSON line per form: calls run, failures (with the first few),
