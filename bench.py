@@ -113,6 +113,56 @@ def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:
     return None
 
 
+def cpu_baseline_pairs(world: int, nbytes: int, iters: int, runs: int) -> dict | None:
+    """The reference itself on the host beside the N >= 2 line: run-hbv3's
+    layout (scripts/run-hbv3.sh:22,28: N ranks, ppn = N/2 flows, -u 1) at the
+    headline's B and iterations, under MPICH shared memory — N/2 concurrent
+    pairs, each a reference process pair on the box's host cores.  A run's
+    aggregate is the pairs' bytes / the slowest sender's time (only group 1
+    writes records, mpi_perf.c:545-554; its time covers its peer's last ack),
+    the reference's implied all-pairs figure; median over runs 1..runs-1 (run 0
+    is the reference's own warm-up, never recorded).  Runs on rank 0 before
+    any GPU call."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not (os.path.exists(ref) and os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libshim.so"))
+            and os.path.exists(mpiexec)):
+        return None
+    ppn = world // 2
+    tmp = tempfile.mkdtemp(prefix="cpu_base_pairs_")
+    try:
+        with open(os.path.join(tmp, "group1"), "w") as f:
+            f.write("localhost\n")
+        os.mkdir(os.path.join(tmp, "logs"))
+        env = dict(os.environ)
+        env.pop("SHIM_OUT", None)
+        cmd = [mpiexec, "-np", str(world), "-genv", "PPN", str(ppn), "-genv", "HOST1", "localhost", "-genv", "HOST0",
+               "127.0.0.1", os.path.join(ROOT, "oracle", "ref_wrap.sh"), ref, "-f", "group1", "-n", "1",
+               "-p", str(ppn), "-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs), "-l", "logs"]
+        p = subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=300)
+        per_run = {}
+        for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log")):
+            for line in open(path):
+                f = line.strip().split(",")
+                per_run.setdefault(int(f[10]), []).append(float(f[9]) / 1000.0)
+        runs_ok = [max(v) for k, v in sorted(per_run.items()) if len(v) == ppn]
+        if p.returncode != 0 or not runs_ok:
+            print(f"[bench] reference pairs baseline failed rc={p.returncode}: {p.stderr[-400:]}", file=sys.stderr)
+            return None
+        t = statistics.median(runs_ok)
+        return dict(value=round(ppn * nbytes * iters / t / 1e9, 3), unit="GB/s", cores=world, kind="reference",
+                    sample=f"mpi_perf.c (oracle/_ref) under MPICH 3.3.2 shm, run-hbv3 layout: {world} ranks, "
+                           f"-p {ppn} -u 1 -b {nbytes} -i {iters} -r {runs} ({ppn} concurrent pairs, one core per "
+                           f"rank); aggregate = {ppn} x B x iters / the slowest sender's time per run, median of runs "
+                           f"1..{runs - 1}",
+                    per_pair_GBps=round(nbytes * iters / t / 1e9, 3), median_run_s=t)
+    except Exception as e:  # noqa: BLE001
+        print(f"[bench] reference pairs baseline unavailable: {e}", file=sys.stderr)
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def traffic_from_profile(workload: str) -> dict | None:
     """Per-launch HBM bytes from the committed PMC summary of this workload
     (profiles/pmc_<workload>.json, written by tools/pmc_summary.py from
@@ -122,6 +172,46 @@ def traffic_from_profile(workload: str) -> dict | None:
         return None
     with open(path) as f:
         return json.load(f)
+
+
+def counters_skip_reason(args) -> str | None:
+    """None when the in-process counters may run; else why not.  A process
+    that rocprofv3 already profiles has its own rocprofiler tool (and
+    dispatch counting serialises kernels): no second one is added."""
+    if args.no_counters:
+        return "--no-counters"
+    for k in ("ROCP_TOOL_LIBRARIES", "ROCPROF_COUNTERS", "ROCPROFILER_LIBRARY_CTOR"):
+        if os.environ.get(k):
+            return f"not sampled in-process: the process runs under a profiler ({k} set)"
+    return None
+
+
+COUNTER_STEPS = 3   # untimed re-run of the headline's steps per counter pass (30 launches of 1 GiB)
+
+
+def copy_traffic(prof, c, src, dst, nbytes: int, iters: int, bus: str) -> dict:
+    """HBM bytes per k_copy launch from this process's own counters: the
+    headline's step re-run COUNTER_STEPS times, untimed, inside a
+    FETCH_SIZE pass and again inside a WRITE_SIZE pass (they cannot share one:
+    TCC has 4 slots, FETCH_SIZE uses 3 and WRITE_SIZE 2, MI355X_MICROARCH.md
+    "PMC slots"); FETCH_SIZE x 2 per the guide's HBM section (gfx950 tallies
+    128-B reads at 64 B), both in KiB."""
+    vals, launches, reset = {}, {}, None
+    for name in ("FETCH_SIZE", "WRITE_SIZE"):
+        n = 0
+        with prof.Pass(bus, [name]) as p:
+            for _ in range(COUNTER_STEPS):
+                n += c.copy(0, dst, src, nbytes, iters).launches
+        vals[name], launches[name], reset = p.values[0], n, p.reads_reset
+    rd = vals["FETCH_SIZE"] * 1024 * 2 / launches["FETCH_SIZE"]
+    wr = vals["WRITE_SIZE"] * 1024 / launches["WRITE_SIZE"]
+    return dict(hbm_read_bytes_per_launch=round(rd, 1), hbm_write_bytes_per_launch=round(wr, 1),
+                hbm_bytes_per_launch=round(rd + wr, 1), traffic_over_algorithmic=round((rd + wr) / (2 * nbytes), 5),
+                launches_per_pass=launches["FETCH_SIZE"], fetch_size_kib=vals["FETCH_SIZE"],
+                write_size_kib=vals["WRITE_SIZE"], reads_reset=reset,
+                source=f"in-process rocprofiler-sdk device counting service (mpi-perf_amd/lib/libmpxprof.so): "
+                       f"FETCH_SIZE x 2 + WRITE_SIZE, separate passes, each over {launches['FETCH_SIZE']} untimed "
+                       f"k_copy launches of this run (the headline's step, {COUNTER_STEPS} times)")
 
 
 def copy_sweep(mpx, c, src, dst, nbytes: int) -> dict:
@@ -292,36 +382,56 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs) -> dic
     return rates
 
 
-LL_AB_SIZES = (1024, 4096, 8192)
-LL_AB_ITERS = 2000
+LL_AB_SIZES = (1024, 2048, 4096, 6144, 8192)
+LL_AB_ITERS, LL_CHECK_ITERS = 2000, 20
+# bytes an LL message writes per payload byte (8-B {tag, 4 B} granules):
+# rocprofv3 --pmc WRITE_SIZE over a 1 KiB LL ping-pong, profiles/r02_pmc_xfer.json
+LL_BYTES_PER_PAYLOAD_BYTE = 2.0
 
 
-def ll_vs_bulk(mpx, torch, dist, c, rounds, rank, tx, rx, errs) -> dict:
-    """Where the LL protocol (data-tagged 8-B granules, one hop) stops paying
-    against bulk (payload + drained flag, 2 B less per granule): round 0's
-    pairs ping-pong at 1, 4 and 8 KiB with every message LL (MPX_LL_MAX =
-    8 KiB, the cross-GPU default) and every message bulk (MPX_LL_MAX = 0),
-    half round trip, max over ranks.  libmpx reads MPX_LL_MAX per call and
-    every rank sets it alike before each loop, so both ends of a pair agree.
-    Kernel engine only; evidence for the cross-GPU `ll_max` choice."""
+def choose_ll_max(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, expect, errs) -> tuple[dict, int]:
+    """The node picks its cross-GPU LL threshold (mpx_xfer_opts has none;
+    libmpx reads MPX_LL_MAX per call), as it picks the push width.  LL: the
+    data is the flag (8-B {tag, 4 B} granules, one link hop, 2 B written per
+    payload byte); bulk: the payload, a drain, then a flag (two hops).
+    Round 0's pairs ping-pong at each LL_AB_SIZES size with every message LL
+    (MPX_LL_MAX = 8192) and every message bulk (MPX_LL_MAX = 0); each form is
+    first run in check mode (every payload checksummed against the peer's
+    tx), then timed: half round trip, max over ranks.  The threshold is the
+    largest size up to which LL is never slower; every rank computes it from
+    the same reduced table.  The caller sets MPX_LL_MAX to it (alike on every
+    rank, so both ends of each pair agree) for everything after."""
     g, peer = round_role(rounds, 0, rank)
+    table = {}
+    sizes = [n for n in LL_AB_SIZES if n <= nbytes]
     old = os.environ.get("MPX_LL_MAX")
-    out = {}
     try:
-        for n in LL_AB_SIZES:
+        for n in sizes:
             for proto, v in (("ll", "8192"), ("bulk", "0")):
                 os.environ["MPX_LL_MAX"] = v
                 dist.barrier()
-                w = torch.tensor([safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, LL_AB_ITERS, tx, rx, n)],
-                                 dtype=torch.float64)
-                dist.all_reduce(w, op=dist.ReduceOp.MAX)
-                out[f"{proto}_{n}"] = finite(float(w[0]) / (2 * LL_AB_ITERS) * 1e6, 3)
+                before = len(errs)
+                safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, LL_CHECK_ITERS, tx, rx, n, check_payload=True,
+                          expect=expect[peer][n])
+                dist.barrier()
+                w = safe_wall(c, errs, mpx.MODE_PINGPONG, g, rank, peer, LL_AB_ITERS, tx, rx, n)
+                if len(errs) > before:
+                    w = float("inf")
+                t = torch.tensor([w], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                table[f"{proto}_{n}"] = finite(float(t[0]) / (2 * LL_AB_ITERS) * 1e6, 3)
     finally:
         if old is None:
             os.environ.pop("MPX_LL_MAX", None)
         else:
             os.environ["MPX_LL_MAX"] = old
-    return out
+    chosen = 512       # LL at <= 512 B is one granule store per lane: never measured slower than bulk
+    for n in sizes:
+        ll, bulk = table.get(f"ll_{n}"), table.get(f"bulk_{n}")
+        if ll is None or bulk is None or ll > bulk:
+            break
+        chosen = n
+    return table, chosen
 
 
 # bulk push variants tuned on the node's own links: (workgroups per push,
@@ -438,19 +548,23 @@ def small_message_check(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes
 HBV3_BYTES, HBV3_ITERS, HBV3_PASSES = 456131, 10, 3
 
 
-def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
+def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs, phases: bool = False) -> dict:
     """run-hbv3's message shape over the all-pairs rounds: every round runs
     the unidir loop at 456131 B x 10 iterations behind a barrier, HBV3_PASSES
     passes; a round's aggregate is pairs x B x iterations / the max over ranks
     of the loop's wall time (the reference's MAX allreduce), median over the
     passes.  At 10 iterations launch and flag latency weigh as much as the
-    link: this is the reference's own short-loop measurement."""
-    walls = []
+    link: this is the reference's own short-loop measurement.  phases (kernel
+    engine): every call's mpx_last_phases split, medians per side over all
+    calls of all ranks (where the fixed cost per call goes)."""
+    walls, ph = [], []
     for _ in range(HBV3_PASSES):
         for rd in range(len(rounds)):
             g, peer = round_role(rounds, rd, rank)
             dist.barrier()
             walls.append(safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES))
+            if phases and walls[-1] != float("inf"):
+                ph.append((g, c.phases(rank)))
     w = torch.tensor(walls, dtype=torch.float64)
     dist.all_reduce(w, op=dist.ReduceOp.MAX)
     nr = len(rounds)
@@ -459,8 +573,16 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
         t = statistics.median(float(w[p * nr + rd]) for p in range(HBV3_PASSES))
         per_round.append(rate((world // 2) * HBV3_BYTES * HBV3_ITERS / 1e9, t, 2))
     ok = [v for v in per_round if v is not None]
-    return dict(bytes=HBV3_BYTES, iters=HBV3_ITERS, round_aggregate_GBps=per_round,
-                mean_aggregate_GBps=round(statistics.mean(ok), 2) if len(ok) == len(per_round) else None)
+    out = dict(bytes=HBV3_BYTES, iters=HBV3_ITERS, round_aggregate_GBps=per_round,
+               mean_aggregate_GBps=round(statistics.mean(ok), 2) if len(ok) == len(per_round) else None)
+    if phases:
+        every = [None] * world
+        dist.all_gather_object(every, ph)
+        allp = [x for e in every for x in (e or [])]
+        out["phases_us_median"] = {
+            side: {k: round(statistics.median(p[k] for gg, p in allp if gg == g) * 1e6, 2) for k in allp[0][1]}
+            for side, g in (("g1", 1), ("g0", 0)) if any(gg == g for gg, _ in allp)} if allp else None
+    return out
 
 
 PULL_AB_ITERS = 100
@@ -511,6 +633,117 @@ def push_vs_pull(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes, nwg, 
     return out
 
 
+def staged_vs_unstaged(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, iters, nwg, stream, expect, expect_ack,
+                       errs) -> dict:
+    """What the headline push reads: each pushing
+    workgroup copies its chunk of tx into LDS once per call and every push
+    reads LDS (tx is read-only while the loop runs; the reference re-sends
+    the same buffer, mpi_perf.c:136).  Round 0's pairs run the headline's
+    unidir loop (B x iters, the tuned width) staged and with
+    MPX_XFER_NOSTAGE (every push reads tx from HBM), each validated first
+    (check mode, 3 iterations); GB/s per pair = B x iters / the max over
+    ranks of the loop's wall time.  On links the two should agree: the link,
+    not the sender's read, bounds the push."""
+    g, peer = round_role(rounds, 0, rank)
+    out = {}
+    for label, stage in (("staged", True), ("unstaged", False)):
+        dist.barrier()
+        before = len(errs)
+        safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, 3, tx, rx, nbytes, check_payload=True, expect=expect,
+                  expect_ack=expect_ack, nwg=nwg, stream=stream, stage=stage)
+        dist.barrier()
+        w = safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream,
+                      stage=stage)
+        if len(errs) > before:
+            w = float("inf")
+        t = torch.tensor([w], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out[f"unidir_{label}_GBps"] = rate(nbytes * iters / 1e9, float(t[0]), 2)
+    return out
+
+
+# xGMI / HBM bytes of the senders, read in-process (mpx/counters.py).  A
+# write to a peer GPU leaves the sender's L2 as an EA write request that is
+# not destined for local DRAM: link requests = WRREQ - WRREQ_DRAM, 64 B each
+# (a bulk push of B bytes makes B / 64 64-B requests: profiles/r02_pmc_xfer_ea.json).
+LINK_COUNTERS = ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum", "TCC_EA0_WRREQ_DRAM_sum")
+READ_COUNTERS = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum")
+
+
+def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes, iters, nwg, stream, buses,
+                  errs) -> dict:
+    """Counters of the timed steps' own work: every round runs once more,
+    untimed (the same loop, width and hint, a barrier per round as in the
+    steps), inside one counter pass per counter set.  The counters are
+    agent-wide, so exactly one rank per GPU samples (the lowest rank on its
+    bus id); on a one-GPU rehearsal that rank sees every pair.  Per G1 launch
+    (N/2 pairs x N-1 rounds launches per pass): link bytes, local-DRAM bytes,
+    EA read requests; rates against the passes' own average G1 launch time."""
+    sampler = rank == min(r for r in range(world) if buses[r] == buses[rank])
+    vals = {}
+    g1_s, g1_n = 0.0, 0
+    notes = []
+    for names in (LINK_COUNTERS, READ_COUNTERS):
+        p = None
+        if sampler:
+            try:
+                p = prof.Pass(buses[rank], list(names)).__enter__()
+            except Exception as e:  # noqa: BLE001
+                notes.append(f"rank {rank}: {type(e).__name__}: {e}"[:200])
+        for rd in range(len(rounds)):
+            g, peer = round_role(rounds, rd, rank)
+            dist.barrier()
+            try:
+                t = c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream)
+                if g == 1 and names is LINK_COUNTERS:
+                    g1_s += t.device_s
+                    g1_n += 1
+            except Exception as e:  # noqa: BLE001
+                errs.append(f"counters: {type(e).__name__}: {e}"[:240])
+        if p is not None:
+            try:
+                p.__exit__(None, None, None)
+                vals.update(zip(names, p.values))
+                vals["reads_reset"] = p.reads_reset
+            except Exception as e:  # noqa: BLE001
+                notes.append(f"rank {rank}: {type(e).__name__}: {e}"[:200])
+    mine = [1.0 if (sampler and all(k in vals for k in LINK_COUNTERS + READ_COUNTERS)) else 0.0]
+    mine += [float(vals.get(k, 0.0)) for k in LINK_COUNTERS + READ_COUNTERS] + [g1_s, float(g1_n)]
+    every = [torch.zeros(len(mine), dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(every, torch.tensor(mine, dtype=torch.float64))
+    all_notes = [None] * world
+    dist.all_gather_object(all_notes, notes)
+    notes = [n for x in all_notes for n in (x or [])]
+    want = sum(1 for r in range(world) if r == min(q for q in range(world) if buses[q] == buses[r]))
+    got = [e for e in every if float(e[0]) == 1.0]
+    if len(got) != want:
+        return {"error": "; ".join(notes) or "not every GPU was sampled", "samplers": want, "sampled": len(got)}
+    tot = [sum(float(e[1 + k]) for e in got) for k in range(len(LINK_COUNTERS) + len(READ_COUNTERS))]
+    wr, w64, dram, rd, rd_dram = tot
+    launches = (world // 2) * len(rounds)
+    alg = nbytes * iters * launches
+    g1_avg = sum(float(e[-2]) for e in every) / max(sum(float(e[-1]) for e in every), 1.0)
+    link = (wr - dram) * 64
+    out = dict(
+        source="in-process rocprofiler-sdk device counting service (mpi-perf_amd/lib/libmpxprof.so), one pass per "
+               "counter set over an untimed re-run of every round (the timed steps' loop, width and hint), one "
+               "sampling rank per GPU",
+        counters=list(LINK_COUNTERS + READ_COUNTERS), samplers=want, g1_launches_per_pass=launches,
+        algorithmic_bytes_per_launch=nbytes * iters,
+        link_bytes_per_launch=round(link / launches, 1),
+        local_dram_write_bytes_per_launch=round(dram * 64 / launches, 1),
+        link_over_algorithmic=round(link / alg, 5), local_dram_over_algorithmic=round(dram * 64 / alg, 5),
+        write_requests_64B_fraction=round(w64 / wr, 5) if wr else None,
+        read_requests_per_launch=round(rd / launches, 1), read_dram_requests_per_launch=round(rd_dram / launches, 1),
+        g1_avg_launch_us=round(g1_avg * 1e6, 2),
+        achieved_link_GBps_per_pair=round(link / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
+        achieved_local_dram_GBps_per_pair=round(dram * 64 / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
+        reads_reset=vals.get("reads_reset"))
+    if notes:
+        out["notes"] = notes
+    return out
+
+
 def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
     """8 B ping-pong half round trip of every pair, round by round
     (PAIR_LATENCY_ITERS iterations each): "g1>g0" -> us, the pair's slower
@@ -534,12 +767,13 @@ def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict
 
 
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                latency=True, tune=True, pull=False) -> dict:
+                latency=True, tune=True, pull=False, prof=None) -> dict:
     """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers;
     pull: the engine's MPX_XFER_PULL form, validation and steps alike).
     Every round's payloads are validated once (check mode, seeded per-rank
-    patterns) before anything is timed.  Returns a dict; "error" is set (on
-    every rank) if any rank failed."""
+    patterns) before anything is timed.  prof (mpx/counters.py, registered):
+    the steps' link / DRAM bytes are counted after them.  Returns a dict;
+    "error" is set (on every rank) if any rank failed."""
     rounds = all_pairs_rounds(world)
     out = {}
     c = None
@@ -558,12 +792,25 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         tx, rx = c.alloc(dev, nbytes), c.alloc(dev, nbytes)
         c.fill(tx, nbytes, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, rank, 0, 0))
         c.attach(rank, dev, tx, rx, nbytes)
-        mine = (c.export(rank), c.checksum(tx, nbytes), c.checksum(tx, 1))
+        # (descriptor, checksums of tx[0:B] and tx[0:1], bus id, checksums of
+        # the small-message and LL-threshold sizes' prefixes)
+        mine = (c.export(rank), c.checksum(tx, nbytes), c.checksum(tx, 1), mpx.bus_id(dev),
+                {n: c.checksum(tx, n) for n in set(SMALL_CHECK_SIZES) | set(LL_AB_SIZES) if n <= nbytes})
     except Exception as e:  # noqa: BLE001
         err = f"rank {rank}: {type(e).__name__}: {e}"[:300]
     descs = [None] * world
     dist.all_gather_object(descs, mine)
     err = agree(err)
+    if engine == "rccl" and not err:
+        # RCCL needs one rank per device; two ranks on one GPU (the one-GPU
+        # rehearsal) are refused here, before ncclCommInitRank: its refused
+        # init left every process of round 3's rehearsal slowed for the rest
+        # of the run (profiles/r03_pull_rounds_diag.jsonl)
+        buses = [d[3] for d in descs]
+        dup = [(a, b) for a in range(world) for b in range(a + 1, world) if buses[a] == buses[b]]
+        if dup:
+            err = (f"RCCL not initialised: ranks {dup[0][0]} and {dup[0][1]} share GPU {buses[dup[0][0]]} "
+                   f"(RCCL needs one rank per device)")
     uid = [None]
     if engine == "rccl" and not err:
         uid = [mpx.rccl_unique_id() if rank == 0 else None]
@@ -642,7 +889,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
             c.prepare(mpx.MODE_UNIDIR, g, rank, peer, iters, nbytes, **pkw)
     for s in range(max(warmup, len(rounds))):
         step(s)
-    dev_s, n_sends = 0.0, 0
+    dev_s, n_sends, step_nwg = 0.0, 0, 0
     step_dev, step_wall = [0.0] * steps, [0.0] * steps   # this rank's G1 device time / wall time per step
     barrier_sync()
     t0 = time.perf_counter()
@@ -655,6 +902,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
             dev_s += t.device_s
             n_sends += 1
             step_dev[s] = t.device_s
+            step_nwg = t.nwg
     barrier_sync()
     elapsed = time.perf_counter() - t0
     err = agree(step_err[0] if step_err else "")
@@ -671,9 +919,24 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     out["per_launch_s"] = float(st[0]) / max(float(st[1]), 1.0)
     out["per_pair_GBps"] = nbytes * iters / out["per_launch_s"] / 1e9
     out.update(pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, nbytes * iters))
+    nw = torch.tensor([float(step_nwg)], dtype=torch.float64)
+    dist.all_reduce(nw, op=dist.ReduceOp.MAX)
+    out["push_nwg"] = int(nw[0])
+    if prof is not None and engine == "kernel":
+        errs = []
+        out["counters"] = link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes, iters, nwg,
+                                        stream, [d[3] for d in descs], errs)
+        if errs:
+            out["counters"]["transfer_errors"] = errs[:3]
+    ll_old = os.environ.get("MPX_LL_MAX")
     if latency:
         # after the headline: a failure here costs its own numbers only
         errs = []
+        if engine == "kernel":
+            # the node's own LL threshold first: everything below runs with it
+            out["ll_vs_bulk_half_rtt_us"], out["ll_max"] = choose_ll_max(
+                mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, [d[4] for d in descs], errs)
+            os.environ["MPX_LL_MAX"] = str(out["ll_max"])
         out["small_message_check"] = small_message_check(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes,
                                                          errs)
         g, peer = round_role(rounds, 0, rank)
@@ -684,11 +947,13 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         out["pingpong_8B_half_rtt_us"] = finite(float(lat[0]) / (2 * LATENCY_ITERS) * 1e6, 3)
         out["pair_pingpong_8B_half_rtt_us"] = pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs)
         out["round0_sweep"] = round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs)
-        if engine == "kernel":
-            out["ll_vs_bulk_half_rtt_us"] = ll_vs_bulk(mpx, torch, dist, c, rounds, rank, tx, rx, errs)
         if nbytes >= HBV3_BYTES:
-            out["hbv3_rounds"] = hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs)
+            out["hbv3_rounds"] = hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs,
+                                             phases=engine == "kernel")
         if engine == "kernel":
+            out["stage"] = staged_vs_unstaged(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, iters, nwg, stream,
+                                              descs[round_role(rounds, 0, rank)[1]][1],
+                                              descs[round_role(rounds, 0, rank)[1]][2], errs)
             # last: a pull failure (e.g. a peer's tx not mapped) breaks only
             # what comes after it on this context
             out["push_vs_pull"] = push_vs_pull(mpx, torch, dist, c, rounds, rank, world, tx, rx, nbytes, nwg, stream,
@@ -697,6 +962,10 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         dist.all_gather_object(every, errs[:3])
         if any(every):
             out["extras_errors"] = {str(r): e for r, e in enumerate(every) if e}
+    if ll_old is None:
+        os.environ.pop("MPX_LL_MAX", None)
+    else:
+        os.environ["MPX_LL_MAX"] = ll_old
     dist.barrier()
     c.close()
     dist.barrier()   # see above: all imports closed before the next allocation
@@ -704,13 +973,13 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
 
 
 def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                        extras: dict, latency: bool = True) -> tuple[dict, str]:
+                        extras: dict, latency: bool = True, prof=None) -> tuple[dict, str]:
     """pairs_bench on `engine`; if the kernel engine fails (payload
     validation, or a device timeout on any rank in validation or in the timed
     steps), measure the SDMA engine instead and say so: an explicit, labelled
     fallback, never a silent one."""
     res = pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                      latency=latency)
+                      latency=latency, prof=prof)
     engine_used = engine
     if res.get("error") and engine == "kernel":
         extras["kernel_engine_error"] = res["error"]
@@ -756,6 +1025,7 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=0, help="transfers per step (default 10 at N=1, 500 at N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-counters", action="store_true", help="no in-process hardware counters (mpx/counters.py)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -776,13 +1046,27 @@ def main() -> None:
         # and the peer's device deadline fires.  One queue per process (the
         # CU-masked rank stream keeps its own) fits.  Set before HIP starts.
         os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
-    # CPU baseline first, before this process touches the GPU
+    # CPU baseline first, before this process touches the GPU: N = 1, two
+    # ranks at 1 GiB (~2.2 s per run on the box: ~13 s of CPU work); N >= 2,
+    # the reference in run-hbv3's layout at the headline's B and iterations
+    # (the other ranks wait in the process-group init meanwhile)
     cpu = None
-    if one and rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(nbytes, 16, 6)   # ~2.2 s per run on the box: ~13 s of CPU work
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(nbytes, 16, 6) if one else cpu_baseline_pairs(world, nbytes, iters, 6)
 
     import torch
     import mpx
+    from mpx import counters
+
+    # In-process counters (roofline.traffic): the tool registers before the
+    # first HIP call of this process (torch is imported, HIP not started yet)
+    prof, prof_note = None, counters_skip_reason(args)
+    if prof_note is None:
+        try:
+            counters.register()
+            prof = counters
+        except counters.CounterError as e:
+            prof_note = f"counters not registered: {e}"
 
     # MPX_BENCH_ONE_GPU=1: rehearse the N>1 path with every rank on GPU 0
     # (two processes on one card share it; the IPC + mailbox path is the same)
@@ -794,6 +1078,10 @@ def main() -> None:
         # library first reads it
         os.environ["MPX_PUSH_WG"] = str(one_gpu_push_cap(world))
     torch.cuda.set_device(dev)
+    torch.cuda.synchronize()                 # HIP (and the counter tool) started
+    if prof is not None and not prof.ready():
+        prof_note = f"counter tool not initialised: {prof.error()}"
+        prof = None
     dist = None
     if not one:
         import datetime
@@ -834,10 +1122,25 @@ def main() -> None:
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=None, kernel="k_copy<1,nt,nt> (one 16-B unit per lane, n/4 KiB blocks)",
                     avg_launch_us=round(per_launch * 1e6, 2), algorithmic_bytes_per_launch=algo)
-        prof = traffic_from_profile(workload)
-        if prof and prof.get("bytes") == nbytes:
-            roof["traffic"] = prof.get("hbm_bytes_per_launch")
-            roof["traffic_source"] = prof.get("source")
+        if prof is not None:
+            try:
+                tr = copy_traffic(prof, c, src, dst, nbytes, iters, mpx.bus_id(0))
+                roof["traffic"] = tr["hbm_bytes_per_launch"]
+                roof["traffic_source"] = tr["source"]
+                roof["traffic_detail"] = tr
+            except Exception as e:  # noqa: BLE001
+                prof_note = f"counter pass failed: {type(e).__name__}: {e}"[:300]
+        committed = traffic_from_profile(workload)
+        if committed and committed.get("bytes") == nbytes:
+            # the rocprofv3 --pmc passes of the same command, committed: the
+            # cross-check of the in-run figure (and the figure when it is off)
+            roof["traffic_rocprofv3"] = dict(hbm_bytes_per_launch=committed.get("hbm_bytes_per_launch"),
+                                             source=committed.get("source"))
+            if roof["traffic"] is None:
+                roof["traffic"] = committed.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = committed.get("source")
+        if prof_note:
+            roof["traffic_note"] = prof_note
         config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine="kernel (k_copy)",
                       parallelism="single GPU")
         metric_unit = "GB/s"
@@ -862,7 +1165,7 @@ def main() -> None:
         # the timed launches as the last ones)
         res, engine_used = pairs_with_fallback(mpx, torch, dist, args.engine, rank, world, dev, nbytes, iters,
                                                args.steps, args.warmup, barrier_sync, extras,
-                                               latency=not args.no_extras)
+                                               latency=not args.no_extras, prof=prof)
         elapsed, total = res["elapsed"], res["total"]
         achieved = res["per_pair_GBps"]
         roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",
@@ -871,16 +1174,35 @@ def main() -> None:
                     frac_of_bidirectional_link=round(achieved / XGMI_LINK_PEAK_BIDIR_GBPS, 4),
                     kernel="k_xfer (G1 side)" if engine_used == "kernel" else engine_used,
                     avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
-        # Link bytes need PMC counters of THIS run's sender launches, which a
-        # process cannot collect on itself: tools/node_profile.sh starts every
-        # rank under its own rocprofv3 (sender TCC_EA0_WRREQ - WRREQ_DRAM, x 64 B
-        # per request) on a multi-GPU node.  A one-GPU loopback constant is no
-        # measurement of an xGMI link, so the line says "not measured".
-        roof["traffic_source"] = ("not measured at N>=2: per-rank link bytes come from tools/node_profile.sh "
-                                  "(rocprofv3 --pmc TCC_EA0_WRREQ/_DRAM per rank)")
+        # Link bytes of THIS run's sender launches, read in-process
+        # (link_counters): per G1 launch, EA write requests not destined for
+        # local DRAM x 64 B.  On the one-GPU rehearsal they are ~0 and the
+        # local-DRAM figure carries the pushes.
+        cnt = res.get("counters")
+        if cnt and "error" not in cnt:
+            roof["traffic"] = cnt["link_bytes_per_launch"]
+            roof["traffic_local_dram"] = cnt["local_dram_write_bytes_per_launch"]
+            roof["traffic_source"] = ("xGMI link bytes per G1 launch: (TCC_EA0_WRREQ - TCC_EA0_WRREQ_DRAM) x 64 B of "
+                                      "every GPU, summed; " + cnt["source"])
+            extras["counters"] = cnt
+        else:
+            roof["traffic_source"] = "not measured: " + ((cnt or {}).get("error") or prof_note or "no counter pass")
+        nwg_used = res.get("push_nwg") or 0
+        chunk = ((-(-nbytes // nwg_used)) + 15) // 16 * 16 if nwg_used else 0
         config = dict(workload=workload, bytes=nbytes, iters_per_step=iters, engine=engine_used,
                       rounds=world - 1, pairs_per_round=world // 2, parallelism=f"pairs{world // 2}",
-                      validated_rounds=res["validated_rounds"], push=res.get("push", "default"))
+                      validated_rounds=res["validated_rounds"], push=res.get("push", "default"),
+                      push_nwg=nwg_used,
+                      # bytes of tx each pushing workgroup holds in LDS (read once per call; 0 = tx read from HBM)
+                      stage=chunk if (engine_used == "kernel" and 0 < chunk <= 60 << 10) else 0)
+        if "ll_max" in res:
+            config["ll_max"] = res["ll_max"]
+            extras["ll_choice"] = dict(chosen_ll_max=res["ll_max"], half_rtt_us=res.get("ll_vs_bulk_half_rtt_us"),
+                                       ll_bytes_written_per_payload_byte=LL_BYTES_PER_PAYLOAD_BYTE,
+                                       rule="largest size up to which LL's half round trip is never above bulk's")
+        if "stage" in res:
+            extras["unidir_staged_vs_unstaged"] = dict(res["stage"], bytes=nbytes, iters=iters)
+            extras["unidir_4MiB_unstaged_GBps"] = res["stage"].get("unidir_unstaged_GBps")
         if res.get("push_tune"):
             extras["push_tune_GBps_per_pair"] = res["push_tune"]
         extras["per_pair_unidir_GBps"] = round(achieved, 2)
@@ -904,8 +1226,6 @@ def main() -> None:
             extras["small_message_check"] = res["small_message_check"]
         if "hbv3_rounds" in res:
             extras["hbv3_rounds_unidir"] = res["hbv3_rounds"]
-        if "ll_vs_bulk_half_rtt_us" in res:
-            extras["ll_vs_bulk_half_rtt_us"] = res["ll_vs_bulk_half_rtt_us"]
         if "push_vs_pull" in res:
             extras["push_vs_pull"] = res["push_vs_pull"]
         if "round0_sweep" in res:
@@ -987,12 +1307,15 @@ def main() -> None:
                 extras["unidir_64MiB_per_pair_GBps"] = round(r3["per_pair_GBps"], 2)
                 extras["unidir_64MiB_pair_GBps_min_max"] = r3.get("pair_GBps_min_max")
                 extras["headline_over_64MiB"] = round(achieved / r3["per_pair_GBps"], 4)
-        # RCCL last: on the one-GPU rehearsal its (refused) communicator init
-        # leaves every process with more streams than the card has hardware
-        # queues, and the co-dependent halves of a pair then share time
-        # slices — every later round ran ~1000x slower there
-        # (profiles/r03_pull_rounds_diag.jsonl)
-        for eng, pull in (("sdma", False), ("kernel", True), ("sdma", True), ("rccl", False)):
+        # RCCL first: pairs_bench refuses it before ncclCommInitRank when two
+        # ranks share a GPU (the one-GPU rehearsal), so no refused init can
+        # slow what follows (round 3 had to run it last:
+        # profiles/r03_pull_rounds_diag.jsonl)
+        try:
+            extras["rccl"] = mpx.rccl_version()   # the RCCL this process runs (torch's, when torch loaded it first)
+        except Exception as e:  # noqa: BLE001
+            extras["rccl"] = f"{type(e).__name__}: {e}"[:200]
+        for eng, pull in (("rccl", False), ("sdma", False), ("kernel", True), ("sdma", True)):
             if not pull and config["engine"].startswith(eng):
                 continue
             # 512 iterations: two graph-replayed SDMA chunks (run_sdma), no host-bound tail

@@ -278,6 +278,11 @@ int mpx_last_phases(mpx_ctx *ctx, int rank, mpx_phases *out);
 int mpx_barrier(mpx_ctx *ctx, int nthreads);
 
 /* ---- RCCL engine setup ---------------------------------------------------- */
+/* The RCCL this process actually runs (ncclGetVersion, e.g. 22707 = 2.27.7)
+   and the file it was loaded from: libmpx links the image's ROCm RCCL, but a
+   process that loaded another librccl.so.1 first (torch bundles its own)
+   resolves libmpx's calls to that one.  len >= 64. */
+int mpx_rccl_version(int *version, char *path, int len);
 int mpx_rccl_get_unique_id(void *id /* MPX_RCCL_ID_BYTES */);
 /* one rank per process (multi-process hosts) */
 int mpx_rccl_init_rank(mpx_ctx *ctx, int rank, int nranks, const void *id);

@@ -20,6 +20,7 @@
 #include <tuple>
 #include <vector>
 
+#include <dlfcn.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -1847,6 +1848,16 @@ int mpx_barrier(mpx_ctx* ctx, int nthreads) {
     } else {
         ctx->bcv.wait(lk, [&] { return ctx->bgen != gen; });
     }
+    return MPX_OK;
+}
+
+int mpx_rccl_version(int* version, char* path, int len) {
+    if (!version || !path || len < 64) return fail(MPX_ERR_INVALID, "bad argument");
+    NCCLCK(ncclGetVersion(version));
+    Dl_info info{};
+    const char* where = dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) && info.dli_fname ? info.dli_fname
+                                                                                                 : "(unknown)";
+    snprintf(path, (size_t)len, "%s", where);
     return MPX_OK;
 }
 

@@ -109,6 +109,7 @@ _SIGS = {
     "mpx_xfer_prepare": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.POINTER(XferOpts)]),
     "mpx_barrier": (C.c_int, [C.c_void_p, C.c_int]),
+    "mpx_rccl_version": (C.c_int, [C.POINTER(C.c_int), C.c_char_p, C.c_int]),
     "mpx_rccl_get_unique_id": (C.c_int, [C.c_void_p]),
     "mpx_rccl_init_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "mpx_rccl_init_all": (C.c_int, [C.c_void_p]),
@@ -275,6 +276,14 @@ class Context:
     def rccl_init_rank(self, rank: int, nranks: int, uid: bytes) -> None:
         buf = C.create_string_buffer(bytes(uid), RCCL_ID_BYTES)
         check(self.L.mpx_rccl_init_rank(self.h, rank, nranks, buf), "mpx_rccl_init_rank")
+
+
+def rccl_version() -> dict:
+    """mpx_rccl_version: the RCCL this process runs and where it came from"""
+    v, buf = C.c_int(0), C.create_string_buffer(512)
+    check(lib().mpx_rccl_version(C.byref(v), buf, 512), "mpx_rccl_version")
+    x = v.value
+    return {"version": x, "release": f"{x // 10000}.{x // 100 % 100}.{x % 100}", "library": buf.value.decode()}
 
 
 def rccl_unique_id() -> bytes:

@@ -26,8 +26,8 @@ rank, scenario = 0, "ok"
 
 
 class Timing:
-    def __init__(self, wall_s, device_s):
-        self.wall_s, self.device_s = wall_s, device_s
+    def __init__(self, wall_s, device_s, nwg=0):
+        self.wall_s, self.device_s, self.nwg = wall_s, device_s, nwg
 
 
 class FakeError(RuntimeError):
@@ -48,6 +48,15 @@ class FakeMpx:
     @staticmethod
     def rccl_unique_id():
         return b"uid-from-rank-0"
+
+    @staticmethod
+    def bus_id(dev):
+        # one GPU per rank, unless the scenario puts every rank on one card
+        return "0000:00:00.0" if scenario in ("one_gpu", "rccl_one_gpu") else f"0000:{rank + 1:02x}:00.0"
+
+    @staticmethod
+    def rccl_version():
+        return {"version": 22707, "release": "2.27.7", "library": "fake"}
 
     class Context:
         def __init__(self, nranks, engine):
@@ -88,7 +97,7 @@ class FakeMpx:
             FakeMpx.log.append(["rccl_init", r, n])
 
         def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,
-                 timeout_ms=0, nwg=0, stream=False, pull=False):
+                 timeout_ms=0, nwg=0, stream=False, pull=False, stage=True):
             if check_payload and self.engine == "kernel" and scenario == "kernel_fails_validation" and rank == 0:
                 raise FakeError("payload checksum mismatch")
             if (scenario == "kernel_step_fails" and self.engine == "kernel" and rank == 1 and mode == 2 and
@@ -97,7 +106,7 @@ class FakeMpx:
             if scenario == "latency_fails" and rank == 1 and mode == 0 and n == 8:
                 raise FakeError("device-side wait timed out (LL ping-pong)")
             FakeMpx.log.append(["xfer", self.engine, mode, group, me, peer, iters, n, bool(check_payload), expect,
-                                expect_ack, nwg, stream, os.environ.get("MPX_LL_MAX"), pull])
+                                expect_ack, nwg, stream, os.environ.get("MPX_LL_MAX"), pull, stage])
             time.sleep(0.002)
             if nwg and not check_payload and iters == 40:
                 # push tuning: rank 0 is fastest at 32, rank 1 slow at 32; the
@@ -107,11 +116,59 @@ class FakeMpx:
                 return Timing(ms * 1e-3, ms * 1e-3)
             return Timing(0.002, 0.001 * (1 + me))
 
+        def phases(self, r):
+            return {k: 1e-6 for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",
+                                      "done_to_return_s")}
+
         def prepare(self, mode, group, me, peer, iters, n, timeout_ms=0, pull=False):
             FakeMpx.log.append(["prepare", self.engine, mode, group, me, peer, iters, n, pull])
 
         def close(self):
             FakeMpx.log.append(["close", self.engine])
+
+
+class FakeProf:
+    """Stand-in for mpx/counters.py: every pass reports fixed counts per
+    counter name (per sampling rank), so the aggregation is checkable."""
+    COUNTS = {"TCC_EA0_WRREQ_sum": 1000.0, "TCC_EA0_WRREQ_64B_sum": 1000.0, "TCC_EA0_WRREQ_DRAM_sum": 10.0,
+              "TCC_EA0_RDREQ_sum": 50.0, "TCC_EA0_RDREQ_DRAM_sum": 5.0}
+    passes = []
+
+    class Pass:
+        def __init__(self, bus, names):
+            self.bus, self.names = bus, names
+            self.values, self.reads_reset = None, 0
+
+        def __enter__(self):
+            FakeProf.passes.append([self.bus, self.names])
+            FakeMpx.log.append(["pass_begin", self.names])
+            return self
+
+        def __exit__(self, *exc):
+            FakeMpx.log.append(["pass_end", self.names])
+            self.values = [FakeProf.COUNTS[n] for n in self.names]
+            return False
+
+
+class FakeCounters:
+    """Stand-in for the mpx.counters module (bench.main: register / ready / Pass)."""
+    CounterError = RuntimeError
+    Pass = FakeProf.Pass
+
+    @staticmethod
+    def register():
+        pass
+
+    @staticmethod
+    def ready():
+        return True
+
+    @staticmethod
+    def error():
+        return ""
+
+
+FakeMpx.counters = FakeCounters
 
 
 if __name__ == "__main__":
@@ -122,9 +179,14 @@ if __name__ == "__main__":
     out = {"rank": rank}
     try:
         nbytes = 65536 if scenario == "tune" else 4096
-        res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, nbytes, 7, 5, 2,
-                                              dist.barrier, extras)
-        out.update(res=res, engine_used=used, extras=extras)
+        if scenario == "rccl_one_gpu":
+            out.update(res=bench.pairs_bench(FakeMpx, torch, dist, "rccl", rank, world, 0, nbytes, 7, 5, 2,
+                                             dist.barrier, latency=False))
+        else:
+            prof = FakeProf if scenario in ("counters", "one_gpu") else None
+            res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, nbytes, 7, 5, 2,
+                                                  dist.barrier, extras, prof=prof)
+            out.update(res=res, engine_used=used, extras=extras, passes=FakeProf.passes)
     except SystemExit as e:
         out.update(exit=str(e))
     out["log"] = FakeMpx.log

@@ -59,8 +59,10 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         checked = [x for x in xf if x[8] and x[2] == 2]
         timed = [x for x in xf if not x[8] and x[2] == 2][:warmup + steps]
         # validation: one checked transfer per round, against the PEER's tx
-        # (then, after the headline, push_vs_pull's two checked unidir loops)
-        assert len(checked) == world - 1 + 2
+        # (then, after the headline, the staged / unstaged pair and
+        # push_vs_pull's two checked unidir loops)
+        assert len(checked) == world - 1 + 2 + 2
+        assert [x[15] for x in checked[world - 1:world + 1]] == [True, False]   # staged, then MPX_XFER_NOSTAGE
         checked = checked[:world - 1]
         for rd, x in enumerate(checked):
             g, peer = round_role(rounds, rd, r)
@@ -69,7 +71,7 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
             assert x[10] == (key(peer) * 31 + 1) & 0xFFFFFFFFFFFFFFFF
         # after the headline: checked ping-pong at the small sizes <= B on
         # every round, each against the peer's tx prefix of that size
-        small = [x for x in xf if x[8] and x[2] == 0]
+        small = [x for x in xf if x[8] and x[2] == 0 and x[7] in (1, 8)]
         sizes = [1, 8]                                        # SMALL_CHECK_SIZES <= B = 4096
         assert len(small) == (world - 1) * len(sizes)
         for i, x in enumerate(small):
@@ -78,6 +80,9 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
             assert (x[3], x[5], x[6], x[7]) == (g, peer, 20, m)
             assert x[9] == (key(peer) * 31 + m) & 0xFFFFFFFFFFFFFFFF
         assert d["res"]["small_message_check"]["failed_transfers"] == 0
+        # the small messages run with the node's chosen LL threshold (the
+        # fake times LL and bulk alike: LL is never slower, so 4 KiB = B)
+        assert d["res"]["ll_max"] == 4096 and all(x[13] == "4096" for x in small)
         # warmup + timed steps: step s runs round s mod (N-1)
         assert len(timed) == warmup + steps
         for s, x in enumerate(timed):
@@ -89,12 +94,14 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
     # per_launch_s averages the G1 launches: G1 rank r reports 0.001*(1+r)
     g1 = [round_role(rounds, s % (world - 1), r)[0] for r in range(world) for s in range(steps)]
     assert sum(g1) == (world // 2) * steps
-    # the ping-pong latency probe ran on round 0 with 10^5 iterations of 8 B,
+    # after the headline: LL against bulk on round 0 (the node's LL threshold),
+    # then the ping-pong latency probe on round 0 with 10^5 iterations of 8 B,
     # then every round's pairs with 10^4, then the round-0 size sweep (config 3: unidir and full-duplex -x 1)
     for d in res:
         r = d["rank"]
         pp_all = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0 and not x[8]]
-        pp, llab = pp_all[:world], pp_all[world:]
+        nll = 2 * 3                                           # LL_AB_SIZES <= B: 1, 2, 4 KiB, LL and bulk
+        llab, pp = pp_all[:nll], pp_all[nll:nll + world]
         assert len(pp) == world and pp[0][6] == 100_000 and pp[0][7] == 8
         # then 10^4 iterations of 8 B on every round: every pair's latency
         for rd, x in enumerate(pp[1:]):
@@ -102,15 +109,19 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         g, peer = round_role(rounds, 0, r)
         sizes = [1, 8, 64, 512, 4096]                        # config 3's sizes <= B (B = 4096 here)
         sweep = [x for x in d["log"] if x[0] == "xfer" and x[1] == "kernel" and not x[8]][
-            warmup + steps + world:warmup + steps + world + 2 * len(sizes)]
+            warmup + steps + nll + world:warmup + steps + nll + world + 2 * len(sizes)]
         assert [x[7] for x in sweep] == [m for m in sizes for _ in (0, 1)]
         assert [x[2] for x in sweep] == [2, 1] * len(sizes)  # -u 1 then -x 1 at every size
         assert all((x[3], x[5]) == (g, peer) for x in sweep)
         assert set(d["res"]["round0_sweep"]) == {f"{m}_{k}" for k in sizes for m in ("unidir", "nonblocking")}
-        # then LL against bulk on round 0: ping-pong at 1/4/8 KiB, MPX_LL_MAX set alike on every rank per loop
-        assert [(x[7], x[13]) for x in llab] == [(m, v) for m in (1024, 4096, 8192) for v in ("8192", "0")]
+        # LL against bulk on round 0: ping-pong at 1/2/4 KiB (<= B), MPX_LL_MAX set alike on every rank per
+        # loop, each form first run in check mode against the peer's tx prefix
+        assert [(x[7], x[13]) for x in llab] == [(m, v) for m in (1024, 2048, 4096) for v in ("8192", "0")]
         assert all((x[3], x[5], x[6]) == (g, peer, 2000) for x in llab)
-        assert set(d["res"]["ll_vs_bulk_half_rtt_us"]) == {f"{p}_{m}" for m in (1024, 4096, 8192) for p in ("ll", "bulk")}
+        llchk = [x for x in d["log"] if x[0] == "xfer" and x[2] == 0 and x[8] and x[7] >= 1024]
+        assert [(x[7], x[13], x[6]) for x in llchk] == [(m, v, 20) for m in (1024, 2048, 4096) for v in ("8192", "0")]
+        assert all(x[9] == (key(peer) * 31 + x[7]) & 0xFFFFFFFFFFFFFFFF for x in llchk)
+        assert set(d["res"]["ll_vs_bulk_half_rtt_us"]) == {f"{p}_{m}" for m in (1024, 2048, 4096) for p in ("ll", "bulk")}
         assert d["ll_max_after"] is None                     # the worker's environment is restored
         # last: push against pull on round 0 at B, each validated (check
         # mode, the peer's expected checksum) before it is timed
@@ -205,5 +216,50 @@ def test_push_tuning_agrees_across_ranks(world, tmp_path):
             assert chk[8] and chk[11] == w and chk[12] == st and (chk[3], chk[5]) == (g, peer)
             assert chk[9] == (key(peer) * 31 + n) & 0xFFFFFFFFFFFFFFFF
             assert not timed[8] and timed[11] == w and timed[12] == st and timed[6] == 40
+        # the warm-up and timed steps, then the staged / unstaged pair (the same loop at B x iters)
         steps_run = [x for x in xf if not x[8] and x[2] == 2 and x[6] == 7]
-        assert len(steps_run) == warmup + steps and all(x[11] == 64 and x[12] for x in steps_run)
+        assert len(steps_run) == warmup + steps + 2 and all(x[11] == 64 and x[12] for x in steps_run)
+        assert [x[15] for x in steps_run] == [True] * (warmup + steps + 1) + [False]
+
+
+def test_rccl_refused_before_init_when_ranks_share_a_gpu(tmp_path):
+    """The one-GPU rehearsal puts every rank on one card: the RCCL engine is
+    refused from the gathered bus ids, on every rank, before any
+    ncclCommInitRank (round 3's refused init slowed every later round of the
+    rehearsal: profiles/r03_pull_rounds_diag.jsonl)."""
+    res = run(2, "rccl_one_gpu", tmp_path)
+    for d in res:
+        assert "share GPU 0000:00:00.0" in d["res"]["error"], d["res"]
+        assert not any(x[0] == "rccl_init" for x in d["log"])
+
+
+@pytest.mark.parametrize("world,scenario", [(2, "counters"), (4, "counters"), (4, "one_gpu")])
+def test_link_counters_one_sampler_per_gpu(world, scenario, tmp_path):
+    """The in-process counter passes (bench.link_counters) after the timed
+    steps: one sampling rank per GPU (the lowest rank on each bus id; all
+    ranks share one on the one-GPU rehearsal), a write pass and a read pass,
+    each around an untimed re-run of every round at the headline's B x iters
+    with the tuned width; per G1 launch, link bytes = (WRREQ - WRREQ_DRAM) x
+    64 summed over the samplers."""
+    res = run(world, scenario, tmp_path)
+    samplers = 1 if scenario == "one_gpu" else world
+    launches = (world // 2) * (world - 1)
+    n, iters = 4096, 7
+    for d in res:
+        cnt = d["res"]["counters"]
+        assert "error" not in cnt, cnt
+        assert cnt["samplers"] == samplers and cnt["g1_launches_per_pass"] == launches
+        assert cnt["link_bytes_per_launch"] == round(samplers * 990 * 64 / launches, 1)
+        assert cnt["local_dram_write_bytes_per_launch"] == round(samplers * 10 * 64 / launches, 1)
+        assert cnt["link_over_algorithmic"] == round(samplers * 990 * 64 / (n * iters * launches), 5)
+        sampled = d["rank"] < samplers
+        assert len(d["passes"]) == (2 if sampled else 0)
+        # each pass wraps exactly one untimed run of every round, after the timed steps
+        log = d["log"]
+        if sampled:
+            b = [i for i, x in enumerate(log) if x[0] == "pass_begin"]
+            e = [i for i, x in enumerate(log) if x[0] == "pass_end"]
+            for i, j in zip(b, e):
+                inside = [x for x in log[i:j] if x[0] == "xfer"]
+                assert len(inside) == world - 1 and all((x[2], x[6], x[7], x[8]) == (2, iters, n, False)
+                                                        for x in inside)

@@ -54,6 +54,18 @@ def test_one_json_line_with_the_contract_keys():
     assert isinstance(d["extras"]["rccl_aggregate_GBps"], float)
     # the comparison engines checksum every round before timing it (config 5)
     assert d["extras"]["sdma_validated_rounds"] == 1 and d["extras"]["rccl_validated_rounds"] == 1
+    assert d["extras"]["rccl"]["release"] == "2.27.7"
+    # the reference itself beside the N >= 2 line: run-hbv3's layout (N ranks,
+    # -p N/2 -u 1) at the headline's B and iterations, under MPICH shm
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["cores"] == 2 and cb["value"] > 0, cb
+    assert "-p 1 -u 1 -b 4194304 -i 500" in cb["sample"]
+    # link bytes from the in-process counters (the stand-in's counts: 990
+    # link requests of 64 B per sampling rank and pass, 2 samplers, 1 launch)
+    assert d["roofline"]["traffic"] == 2 * 990 * 64 and d["extras"]["counters"]["samplers"] == 2
+    assert d["config"]["ll_max"] == 8192 and d["extras"]["ll_choice"]["chosen_ll_max"] == 8192
+    assert d["extras"]["unidir_4MiB_unstaged_GBps"] is not None
+    assert d["extras"]["hbv3_rounds_unidir"]["phases_us_median"]["g1"]["kernel_s"] == 1.0
 
 
 def test_hung_comparison_engine_cannot_cost_the_line():
@@ -63,8 +75,10 @@ def test_hung_comparison_engine_cannot_cost_the_line():
     assert len(got) == 1
     d = got[0]
     assert d["extras"]["comparison_engines"] == "abandoned after 5 s"
-    assert isinstance(d["extras"]["sdma_aggregate_GBps"], float)      # finished before RCCL hung
-    assert "rccl_aggregate_GBps" not in d["extras"]
+    # RCCL runs first among the comparison engines: nothing after it ran, but
+    # the headline and everything measured before the watchdog are in the line
+    assert "rccl_aggregate_GBps" not in d["extras"] and "sdma_aggregate_GBps" not in d["extras"]
+    assert d["value"] > 0 and d["extras"]["counters"]["samplers"] == 2
 
 
 def test_every_pair_of_four_ranks_has_a_rate():
