@@ -189,6 +189,11 @@ int mpx_device_bus_id(int dev, char *buf, int len);
 int mpx_init(int nranks, int engine, mpx_ctx **ctx);
 /* MPI_Finalize analogue (mpi_perf.c:581) */
 int mpx_finalize(mpx_ctx *ctx);
+/* After the last mpx_finalize: destroy the process-lifetime rank streams
+   (mpx_finalize returns them to a per-device pool) while the process is
+   fully alive, instead of leaving them to the HIP runtime's exit teardown.
+   MPX_ERR_STATE while a context is alive. */
+int mpx_shutdown(void);
 
 /* ---- buffers (allocate_tx_rx_buffers, mpi_perf.c:240-252) ---------------- */
 /* posix_memalign(4096) analogue: device memory on `dev`, 4 KiB aligned.  The

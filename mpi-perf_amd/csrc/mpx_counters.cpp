@@ -23,6 +23,10 @@
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -190,7 +194,24 @@ int sample(std::vector<double>& out) {
 
 extern "C" {
 
+// Diagnostics: a process that registers the tool and later dies of SIGSEGV
+// prints the faulting thread's native stack to stderr first (then the default
+// action runs), so an exit-time crash names the library it happened in.
+void segv_dump(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "[mpxprof] fatal signal; native stack:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int mpxprof_register(void) {
+    if (getenv("MPXPROF_SEGV_DUMP")) {
+        signal(SIGSEGV, segv_dump);
+        signal(SIGABRT, segv_dump);
+    }
     const rocprofiler_status_t s = rocprofiler_force_configure(&tool_configure);
     if (s != ROCPROFILER_STATUS_SUCCESS) return fail("rocprofiler_force_configure: %s", rocprofiler_get_status_string(s));
     return 0;

@@ -1830,6 +1830,24 @@ int mpx_xfer(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, i
     return st;
 }
 
+int mpx_shutdown(void) {
+    StreamPool& p = pool();
+    std::lock_guard<std::mutex> lk(p.mu);
+    if (p.live_contexts != 0) return fail(MPX_ERR_STATE, "%d contexts are still alive", p.live_contexts);
+    if (p.all.empty()) return MPX_OK;
+    callback_fence(p.all);
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (auto& ds : p.all) {
+        (void)hipSetDevice(ds.first);
+        HIPCK(hipStreamDestroy(ds.second));
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    p.all.clear();
+    p.idle.clear();
+    return MPX_OK;
+}
+
 int mpx_last_phases(mpx_ctx* ctx, int rank, mpx_phases* out) {
     if (!ctx || !out) return fail(MPX_ERR_INVALID, "NULL argument");
     if (rank < 0 || rank >= ctx->nranks || !ctx->r[rank].local) return fail(MPX_ERR_STATE, "rank %d is not a local rank", rank);

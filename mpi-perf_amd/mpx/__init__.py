@@ -93,6 +93,7 @@ _SIGS = {
     "mpx_last_phases": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Phases)]),
     "mpx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "mpx_finalize": (C.c_int, [C.c_void_p]),
+    "mpx_shutdown": (C.c_int, []),
     "mpx_alloc": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]),
     "mpx_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mpx_fill": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_int, C.c_uint64]),
@@ -162,6 +163,11 @@ def link_info(dev_a: int, dev_b: int) -> dict:
     t, h = C.c_int(0), C.c_int(0)
     check(lib().mpx_link_info(dev_a, dev_b, C.byref(t), C.byref(h)), "mpx_link_info")
     return {"type": LINK_TYPES.get(t.value, t.value), "hops": h.value}
+
+
+def shutdown() -> None:
+    """mpx_shutdown: destroy the pooled rank streams (no context alive)."""
+    check(lib().mpx_shutdown(), "mpx_shutdown")
 
 
 def bus_id(dev: int) -> str:

@@ -5,7 +5,10 @@ committed in profiles/pmc_local_d2d_copy.json (k_copy 1 GiB: 1.0004 x
 algorithmic) and profiles/r02_pmc_xfer_ea.json (a loopback push writes one
 64-B request per 64 B pushed, all to local DRAM)?
 
-    python tools/counters_probe.py torch_first | prof_first | no_torch
+    python tools/counters_probe.py torch_first | prof_first | no_torch [shutdown] [nopair]
+
+shutdown: mpx_shutdown() (pooled rank streams destroyed) before exit.
+nopair: the copy passes only (no rank attached: no rank streams exist).
 
 Prints one JSON line.
 """
@@ -69,9 +72,9 @@ with mpx.Context(2, "kernel") as c:
     c.free(src)
     c.free(dst)
     # a loopback pair (two ranks on GPU 0, one thread each): unidir 4 MiB x 500
-    B, IT = 4 << 20, 500
+    B, IT = 4 << 20, (0 if "nopair" in sys.argv[2:] else 500)
     bufs = []
-    for r in range(2):
+    for r in range(2 if IT else 0):
         tx, rx = c.alloc(0, B), c.alloc(0, B)
         c.fill(tx, B, mpx.FILL_SPLITMIX, r + 1)
         c.attach(r, 0, tx, rx, B)
@@ -92,8 +95,10 @@ with mpx.Context(2, "kernel") as c:
             x.join()
         assert not errs, errs
 
-    run_pair(20)
+    if IT:
+        run_pair(20)
     try:
+        assert IT, "nopair: no rank streams in this process"
         with counters.Pass(bus, ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum", "TCC_EA0_WRREQ_DRAM_sum"]) as p:
             run_pair(IT)
         wr, w64, dram = p.values
@@ -103,4 +108,7 @@ with mpx.Context(2, "kernel") as c:
                                             link_req=wr - dram)
     except Exception as e:  # noqa: BLE001
         out["pair_unidir_4MiB_x500"] = f"{type(e).__name__}: {e}"
+if "shutdown" in sys.argv[2:]:
+    mpx.shutdown()
+    out["shutdown"] = "pooled rank streams destroyed before exit"
 print(json.dumps(out), flush=True)
