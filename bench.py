@@ -344,6 +344,20 @@ def safe_wall(c, errs: list, *xfer_args, **xfer_kw) -> float:
         return float("inf")
 
 
+def arm(c, errs: list, *xfer_args, **xfer_kw) -> bool:
+    """mpx_xfer_arm ahead of the barrier: the transfer's kernel is launched
+    now and started by the xfer call with the same arguments after the
+    barrier (MPI's persistent-request split, include/mpx.h), so the ~14 us
+    launch is not inside the timed call.  A failure to arm is recorded and
+    the call then launches inline."""
+    try:
+        c.arm(*xfer_args, **xfer_kw)
+        return True
+    except Exception as e:  # noqa: BLE001
+        errs.append(f"arm: {type(e).__name__}: {e}"[:240])
+        return False
+
+
 def finite(x: float, digits: int):
     return round(x, digits) if x != float("inf") and x == x else None
 
@@ -368,6 +382,7 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs) -> dic
     rates = {}
 
     def timed(mode, n, it):
+        arm(c, errs, mode, g, rank, peer, it, tx, rx, n, timeout_ms=POST_TIMEOUT_MS)
         dist.barrier()
         w = torch.tensor([safe_wall(c, errs, mode, g, rank, peer, it, tx, rx, n)], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
@@ -554,13 +569,15 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs, phases: 
     passes; a round's aggregate is pairs x B x iterations / the max over ranks
     of the loop's wall time (the reference's MAX allreduce), median over the
     passes.  At 10 iterations launch and flag latency weigh as much as the
-    link: this is the reference's own short-loop measurement.  phases (kernel
+    link: this is the reference's own short-loop measurement.  Each call is
+    armed before its barrier (arm), as the timed steps are.  phases (kernel
     engine): every call's mpx_last_phases split, medians per side over all
     calls of all ranks (where the fixed cost per call goes)."""
     walls, ph = [], []
     for _ in range(HBV3_PASSES):
         for rd in range(len(rounds)):
             g, peer = round_role(rounds, rd, rank)
+            arm(c, errs, mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES, timeout_ms=POST_TIMEOUT_MS)
             dist.barrier()
             walls.append(safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES))
             if phases and walls[-1] != float("inf"):
@@ -580,7 +597,8 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs, phases: 
         dist.all_gather_object(every, ph)
         allp = [x for e in every for x in (e or [])]
         out["phases_us_median"] = {
-            side: {k: round(statistics.median(p[k] for gg, p in allp if gg == g) * 1e6, 2) for k in allp[0][1]}
+            side: {k: round(statistics.median(p[k] for gg, p in allp if gg == g) * 1e6, 2) for k in allp[0][1]
+                   if k != "armed"}
             for side, g in (("g1", 1), ("g0", 0)) if any(gg == g for gg, _ in allp)} if allp else None
     return out
 
@@ -870,8 +888,14 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
 
     def step(s: int):
         g, peer = round_role(rounds, s % len(rounds), rank)
+        # the step's kernel is launched ahead of the barrier and started after
+        # it (mpx_xfer_arm; a no-op on the SDMA and RCCL engines)
+        armed = not step_err and arm(c, step_err, mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg,
+                                     stream=stream, **pkw)
         dist.barrier()                               # MPI_Barrier, mpi_perf.c:499
         if step_err:                                 # keep joining the barriers, transfer nothing
+            if armed:
+                c.disarm(rank)
             return g, None
         try:
             return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream, **pkw)
@@ -1337,6 +1361,11 @@ def main() -> None:
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    # every context is finalized: the pooled rank streams go now, while the
+    # process is whole — left to the exit teardown, they made the counter
+    # tool's (rocprofiler-sdk's) exit-time finalizer fault in libhsa-runtime64
+    # (profiles/r04_exit_segv_stack.txt)
+    mpx.shutdown()
 
 
 if __name__ == "__main__":

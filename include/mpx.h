@@ -245,6 +245,23 @@ int mpx_xfer(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, i
 int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
                 void *tx, void *rx, int buff_len, const mpx_xfer_opts *opts, mpx_timing *t);
 
+/* Arm the next transfer of my_rank (kernel engine): its kernel is launched
+   now and waits on the device; the next mpx_xfer_ex with the SAME arguments
+   starts it with one store into host-mapped memory and times only that
+   start and the loop.  MPI's persistent requests split a transfer the same
+   way (MPI_Send_init / MPI_Recv_init before, MPI_Start inside the timed
+   region); hosts arm before their barrier (mpi_perf.c:499), so the kernel
+   launch (~14 us on MI355X, profiles/r04_phases_query.jsonl) is no longer
+   part of every short loop's recorded time.  The armed call's device_s is
+   the kernel's own clock from start to end.  A rank holds one armed call;
+   mpx_xfer_ex with other arguments fails (MPX_ERR_STATE) and leaves it
+   armed.  The SDMA and RCCL engines accept the call and do nothing. */
+int mpx_xfer_arm(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
+                 void *tx, void *rx, int buff_len, const mpx_xfer_opts *opts);
+/* Cancel an armed call that will not be started (no transfer happens);
+   mpx_finalize does it for every armed rank. */
+int mpx_xfer_disarm(mpx_ctx *ctx, int my_rank);
+
 /* Build, outside any timed region, what a later mpx_xfer_ex with the same
    (mode, group, ranks, iters, buff_len, opts) would otherwise build on its
    first call: the SDMA engine's graph-captured loop chunks, or the RCCL
@@ -274,6 +291,10 @@ typedef struct mpx_phases {
     double kernel_s;          /* first workgroup start -> last workgroup end    */
     double done_to_return_s;  /* completion word seen -> the kernel retired and
                                  the call returned                              */
+    int32_t armed;            /* 1: the call was armed (mpx_xfer_arm): its
+                                 launch happened before the call, and
+                                 launch_to_start_s is go store -> running       */
+    int32_t reserved;
 } mpx_phases;
 int mpx_last_phases(mpx_ctx *ctx, int rank, mpx_phases *out);
 

@@ -77,7 +77,11 @@ struct Status {
     u64 t_exit;             // the last workgroup finished
     u64 done;               // XferArgs.done_token, stored by the last workgroup
                             // after everything else (the host's completion word)
+    u64 go;                 // armed call (mpx_xfer_arm): the host stores the
+                            // call's token here to start it, token | kGoCancel
+                            // to end it without a transfer
 };
+constexpr u64 kGoCancel = 1ull << 63;
 
 // Device scratch words of a rank ([0..3]: zero when a kernel-engine call
 // starts — zeroed at attach, and reset by the last workgroup of every call, so
@@ -85,8 +89,11 @@ struct Status {
 //   [0] grid-barrier counter  [1] abort word  [2] finished workgroups
 //   [3] pull mode: chunks landed in rx this call (all receives, all workgroups)
 //   [4..5] SDMA engine's device-side sequence base {tx, rx}
-constexpr int kScratchWords = 8;
-constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrLanded = 3, kScrSeqBase = 4, kScrLink = 6;
+//   [6..7] RCCL engine's one-byte link set-up exchange
+//   [8] armed call: workgroup 0's go verdict for the others (1 go, 2 cancel),
+//       reset with [0..3]
+constexpr int kScratchWords = 16;
+constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrLanded = 3, kScrSeqBase = 4, kScrLink = 6, kScrGo = 8;
 
 // Non-blocking check mode ("ring"): receive j of a call with `iters`
 // iterations lands in slot (iters-1-j) mod S of the receiver, where slot 0 is
@@ -147,6 +154,9 @@ struct XferArgs {
     int no_pull_wait;            // test knob (MPX_TEST_NO_PULL_WAIT): a sending side
                                  // ends without waiting for the peer's loads of tx
     u64 done_token;              // stored into Status.done by the last workgroup
+    u64 go_token;                // armed call: wait for Status.go == go_token first
+                                 // (0: start at once)
+    u64 go_timeout_ticks;        // armed call: how long the kernel waits for go
 };
 
 // LL threshold of a link.  Within one GPU the bulk path's extra hop (payload

@@ -631,15 +631,22 @@ struct Loop {
                 __builtin_amdgcn_s_sleep(0);
             }
             if (blockIdx.x == 0 && !*s_abort) {
+                // write-through (sc0 sc1) like every other store into rx, so
+                // the bytes are in memory once the call's completion word is
+                const __amdgpu_buffer_rsrc_t rr = rsrc(a.rx, (unsigned)n);
 #pragma unroll
                 for (int j = 0; j < kLLUnitsPerLane; ++j) {
                     if (j >= mine) break;
                     const long long off = 8ll * ((int)threadIdx.x + j * kBlock);
                     const u64 d = ((u64)x[j].z << 32) | x[j].x;
                     if (off + 8 <= n) {
-                        *reinterpret_cast<u64*>(a.rx + off) = d;
+                        const unsigned lo = (unsigned)d, hi = (unsigned)(d >> 32);
+                        __builtin_amdgcn_raw_buffer_store_b32(lo, rr, (unsigned)off, 0, kAuxSys);
+                        __builtin_amdgcn_raw_buffer_store_b32(hi, rr, (unsigned)off + 4, 0, kAuxSys);
                     } else {
-                        for (long long b = 0; off + b < n; ++b) a.rx[off + b] = (unsigned char)(d >> (8 * b));
+                        for (long long b = 0; off + b < n; ++b)
+                            __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(d >> (8 * b)), rr, (unsigned)(off + b),
+                                                                 0, kAuxSys);
                     }
                 }
             }
@@ -708,13 +715,29 @@ struct Loop {
         const bool last = iter + 1 == a.iters;
         u64 acc = 0;
         if (is_ll(n)) {
-            // unpacked by workgroup 0 with plain stores: same-workgroup reads
+            // unpacked by workgroup 0 with write-through stores: read back
+            // the same way (sc0 sc1 loads: no L1 line of an earlier
+            // iteration's read can serve them)
             if (blockIdx.x == 0) {
-                for (long long k = threadIdx.x; 8 * k < n; k += kBlock)
-                    acc += csum_term(tail_word(a.rx, 8 * k, n), k);
+                const __amdgpu_buffer_rsrc_t rr = rsrc(a.rx, (unsigned)n);
+                for (long long k = threadIdx.x; 8 * k < n; k += kBlock) {
+                    const unsigned o = (unsigned)(8 * k);
+                    u64 w = 0;
+                    if (8 * k + 8 <= n) {
+                        w = (u64)__builtin_amdgcn_raw_buffer_load_b32(rr, o, 0, kAuxSys) |
+                            ((u64)__builtin_amdgcn_raw_buffer_load_b32(rr, o + 4, 0, kAuxSys) << 32);
+                    } else {
+                        for (long long b = 0; 8 * k + b < n; ++b)
+                            w |= (u64)__builtin_amdgcn_raw_buffer_load_b8(rr, o + (unsigned)b, 0, kAuxSys) << (8 * b);
+                    }
+                    acc += csum_term(w, k);
+                }
                 __syncthreads();
-                if (!last)
-                    for (long long o = threadIdx.x; o < n; o += kBlock) a.rx[o] = (unsigned char)poison;
+                if (!last) {
+                    for (long long o = threadIdx.x; o < n; o += kBlock)
+                        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)poison, rr, (unsigned)o, 0, kAuxSys);
+                    drain_stores();   // the poison lands before the next payload's unpack
+                }
             }
         } else if ((int)blockIdx.x < a.nwg) {
             acc = sum_chunk(a.rx, n, poison, last);
@@ -783,6 +806,46 @@ struct Loop {
         }
     }
 
+    // ---- armed calls (mpx_xfer_arm) ----------------------------------------
+    // The kernel was launched before the host's barrier; the loop starts when
+    // the host stores this call's token into Status.go (mpx_xfer_ex after the
+    // barrier) — MPI's persistent-request split (MPI_Send_init ... MPI_Start).
+    // Workgroup 0 polls the host word and hands its verdict to the others in
+    // scratch word kScrGo.  False: cancelled (mpx_xfer_disarm) or no start
+    // within go_timeout_ticks (then Status.err = 2): no transfer at all.
+    __device__ bool wait_go() const {
+        if (!a.go_token) return true;
+        __shared__ int s_go;
+        if (threadIdx.x == 0) {
+            const u64 t0 = now_ticks();
+            u64 spins = 0, w = 0;
+            if (blockIdx.x == 0) {
+                for (;;) {
+                    const u64 v = ld_sys(&a.status->go);
+                    if (v == a.go_token) { w = 1; break; }
+                    if (v == (a.go_token | kGoCancel)) { w = 2; break; }
+                    if ((++spins & 63) == 0 && now_ticks() - t0 > a.go_timeout_ticks) {
+                        __hip_atomic_store(&a.status->err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        w = 2;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __hip_atomic_store(&a.gbar[kScrGo], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                // (workgroup 0 answers within its own deadline; one second
+                // more bounds this wait should it never run)
+                while ((w = __hip_atomic_load(&a.gbar[kScrGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                    if ((++spins & 63) == 0 && now_ticks() - t0 > a.go_timeout_ticks + 100000000ull) { w = 2; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            s_go = (int)w;
+        }
+        __syncthreads();
+        return s_go == 1;
+    }
+
     // ---- call phases and the end of the call --------------------------------
     // Workgroup 0 stamps the call's start (Status.t_entry) as its first action
     // and, on a side that pushes first, the moment the peer's receives were
@@ -810,6 +873,7 @@ struct Loop {
     __device__ void finish_last() const {
         if (threadIdx.x != 0) return;
         for (int k = 0; k < 4; ++k) __hip_atomic_store(&a.gbar[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.gbar[kScrGo], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         st_sys(&a.status->t_exit, now_ticks());
         drain_stores();
         st_sys(&a.status->done, a.done_token);
@@ -1079,6 +1143,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     extern __shared__ v4u s_tx[];            // a.stage: dynamic LDS = one chunk
     if (threadIdx.x == 0) s_abort = 0;
     Loop<MODE> L{a, &s_abort, lds4, s_tx, {}};
+    if (!L.wait_go()) {
+        if (L.last_to_finish()) L.finish_last();
+        return;
+    }
     L.stamp(&a.status->t_entry);
     const long long n = a.len;
     if (a.stage) L.stage_tx(n);
@@ -1175,6 +1243,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     extern __shared__ v4u s_tx[];
     if (threadIdx.x == 0) s_abort = 0;
     Loop<MPX_MODE_NONBLOCKING> L{a, &s_abort, lds4, s_tx, {}};
+    if (!L.wait_go()) {
+        if (L.last_to_finish()) L.finish_last();
+        return;
+    }
     L.stamp(&a.status->t_entry);
     const long long n = a.len;
     if (a.stage) L.stage_tx(n);
@@ -1246,6 +1318,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
         s_seen = 0;
     }
     Loop<MODE> L{a, &s_abort, lds4, nullptr, {}, &s_seen};
+    if (!L.wait_go()) {
+        if (L.last_to_finish()) L.finish_last();
+        return;
+    }
     L.stamp(&a.status->t_entry);
     const long long n = a.len;
     const u64 nw = (u64)a.nwg;

@@ -112,6 +112,7 @@ struct Rank {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     u64 token = 0;                 // kernel-engine calls made: Status.done of the last one
     mpx_phases phases{};           // the last kernel-engine call (mpx_last_phases)
+    struct KernelCall* armed = nullptr;   // the call mpx_xfer_arm launched, not started yet
     Status* status = nullptr;      // host-mapped (local ranks)
     u64* scratch = nullptr;        // kScratchWords device words (local ranks)
     u64* csum = nullptr;           // per-iteration checksums (device), csum_cap words,
@@ -580,22 +581,49 @@ int sync_mode() {
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
 
-// Wait until the call's kernel (end event ev1) has completed; *t_done = the
-// host time the completion word was first seen (0 in event mode).
-int wait_kernel(Rank& me, u64 token, double* t_done) {
+// One kernel-engine call: its arguments and launch shape, built by
+// prepare_call; launched at once (run_kernel) or armed ahead of the host's
+// barrier (mpx_xfer_arm) and started later (mpx_xfer_ex).
+struct KernelCall {
+    XferArgs a{};
+    int grid = 0;
+    bool ll = false;
+    int my_rank = 0, peer_rank = 0, mode = 0, group = 0, iters = 0;
+    long long len = 0;
+    // what an armed call was armed with: mpx_xfer_ex must match it
+    int check = 0, flags = 0, nwg_opt = 0;
+    uint32_t timeout_ms = 0;
+    uint64_t expect = 0, expect_ack = 0;
+    double t_launch = 0;
+};
+
+// Wait for the call's completion.  Unarmed: the end event ev1 (see
+// sync_mode); *t_done = when the completion word was first seen (0 in event
+// mode).  Armed: the completion word only — every byte the kernel leaves for
+// the host or another stream (rx included: LL unpacks are write-through) is
+// in memory before it is stored; the stream is polled every 50 us so that a
+// kernel that ended without storing it (it cannot, but a fault could) ends
+// the wait with an error instead of a hang.
+int wait_kernel(Rank& me, u64 token, bool armed, double* t_done) {
     *t_done = 0;
-    if (sync_mode() == kSyncEvent) {
+    if (!armed && sync_mode() == kSyncEvent) {
         HIPCK(hipEventSynchronize(me.ev1));
         return MPX_OK;
     }
-    // Before the word arrives the end event is polled only every 50 us (a
-    // kernel that could not launch never stores it); after, back to back.
+    // Before the word arrives the end event / stream is polled only every
+    // 50 us (a kernel that could not launch never stores it); after, back to
+    // back (unarmed) or not at all (armed).
     double next_query = now_s() + 50e-6;
     for (;;) {
-        if (*t_done == 0 && __atomic_load_n(&me.status->done, __ATOMIC_ACQUIRE) == token) *t_done = now_s();
+        if (*t_done == 0 && __atomic_load_n(&me.status->done, __ATOMIC_ACQUIRE) == token) {
+            *t_done = now_s();
+            if (armed) return MPX_OK;
+        }
         if (*t_done != 0 || now_s() >= next_query) {
-            const hipError_t q = hipEventQuery(me.ev1);
+            const hipError_t q = armed ? hipStreamQuery(me.stream) : hipEventQuery(me.ev1);
             if (q == hipSuccess) {
+                if (armed && __atomic_load_n(&me.status->done, __ATOMIC_ACQUIRE) != token)
+                    return fail(MPX_ERR_HIP, "armed transfer kernel ended without its completion word");
                 if (*t_done == 0) *t_done = now_s();
                 return MPX_OK;
             }
@@ -606,10 +634,10 @@ int wait_kernel(Rank& me, u64 token, double* t_done) {
     }
 }
 
-int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters,
-               long long len, const mpx_xfer_opts* o, mpx_timing* t) {
-    const double t_call = now_s();
-    XferArgs a{};
+int prepare_call(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters,
+                 long long len, const mpx_xfer_opts* o, KernelCall* kc) {
+    XferArgs& a = kc->a;
+    a = XferArgs{};
     a.tx = me.tx;
     a.rx = me.rx;
     a.peer_rx = peer.rx;
@@ -679,8 +707,7 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     }
     if (!a.pull && a.check && mode == MPX_MODE_NONBLOCKING && len > 0 && a.slots > 1 && (!a.ring || !a.peer_ring))
         return fail(MPX_ERR_STATE, "rank %d/%d: check-mode receive ring missing", my_rank, peer_rank);
-    const int grid = a.pull ? (recvs_len ? a.nwg : 1)
-                            : (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;
+    kc->grid = a.pull ? (recvs_len ? a.nwg : 1) : (!ll && (pushes_len || (a.check && recvs_len))) ? a.nwg : 1;
     // bulk pushes read tx from LDS when one workgroup's chunk fits
     // (kStageMaxBytes); the call's MPX_XFER_NOSTAGE flag reads it from HBM
     if (!(o && (o->flags & MPX_XFER_NOSTAGE)) && !ll && !a.pull && pushes_len && len > 0) {
@@ -694,64 +721,132 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
         const long long chunk = (((len + a.nwg - 1) / a.nwg) + 15) & ~15ll;
         if (chunk <= kStageMaxBytes && chunk <= lds_cap) a.stage = (int)chunk;
     }
+    a.done_token = ++me.token;
+    // a call that moves nothing (iters = 0) posts nothing new: the count
+    // stays equal on both sides even if only one side makes such a call
+    a.call = iters > 0 ? ++me.calls[peer_rank] : me.calls[peer_rank];
+    if (knobs.no_posted) a.call = 0;   // every wait for posted >= 0 holds at once
+    kc->ll = ll;
+    kc->my_rank = my_rank;
+    kc->peer_rank = peer_rank;
+    kc->mode = mode;
+    kc->group = group;
+    kc->iters = iters;
+    kc->len = len;
+    kc->check = a.check;
+    kc->flags = o ? o->flags : 0;
+    kc->nwg_opt = o ? o->nwg : 0;
+    kc->timeout_ms = o ? o->timeout_ms : 0;
+    kc->expect = o ? o->expect_checksum : 0;
+    kc->expect_ack = o ? o->expect_ack : 0;
+    return MPX_OK;
+}
 
-    // (scratch words [0..3] are zero: the previous call's last workgroup
-    // reset them — no memset on the stream ahead of the kernel)
+// Enqueue the call's kernel on the rank's stream (scratch words [0..3] and
+// [8] are zero: the previous call's last workgroup reset them — no memset
+// ahead of the kernel).  Armed: go_token set, no events (the kernel's span
+// comes from its own clock).
+int launch_call(Rank& me, KernelCall& kc, bool armed) {
+    XferArgs& a = kc.a;
     if (a.check) {
-        HIPCK(hipMemsetAsync(me.csum, 0, (size_t)iters * sizeof(u64), me.stream));
-        if (mode == MPX_MODE_NONBLOCKING) HIPCK(hipMemsetAsync(me.cnt, 0, (size_t)iters * sizeof(u64), me.stream));
+        HIPCK(hipMemsetAsync(me.csum, 0, (size_t)kc.iters * sizeof(u64), me.stream));
+        if (kc.mode == MPX_MODE_NONBLOCKING)
+            HIPCK(hipMemsetAsync(me.cnt, 0, (size_t)kc.iters * sizeof(u64), me.stream));
     }
     me.status->err = 0;
     me.status->where = 0;
     me.status->recv_done = 0;
     me.status->recv_digest = 0;
     me.status->t_entry = me.status->t_posted = me.status->t_exit = 0;
-    a.done_token = ++me.token;
-
-    // a call that moves nothing (iters = 0) posts nothing new: the count
-    // stays equal on both sides even if only one side makes such a call
-    a.call = iters > 0 ? ++me.calls[peer_rank] : me.calls[peer_rank];
-    if (knobs.no_posted) a.call = 0;   // every wait for posted >= 0 holds at once
-    const double t0 = now_s();
+    if (armed) {
+        a.go_token = a.done_token;
+        // the host's barrier sits between arm and start: bounded generously
+        a.go_timeout_ticks = std::max<u64>(a.timeout_ticks, 60ull * 100000000ull);
+        kc.t_launch = now_s();
+        HIPCK(launch_xfer(a, kc.grid, me.stream));
+        return MPX_OK;
+    }
+    kc.t_launch = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
-    HIPCK(launch_xfer(a, grid, me.stream));
+    HIPCK(launch_xfer(a, kc.grid, me.stream));
     HIPCK(hipEventRecord(me.ev1, me.stream));
+    return MPX_OK;
+}
+
+// Wait for the call, then its timing, phases and receive accounting.  t0 =
+// the start of the timed call: the launch (unarmed) or the go store (armed).
+int complete_call(Rank& me, KernelCall& kc, bool armed, double t_call, double t0, mpx_timing* t) {
+    XferArgs& a = kc.a;
     double t_done = 0;
-    TRY(wait_kernel(me, a.done_token, &t_done));
+    TRY(wait_kernel(me, a.done_token, armed, &t_done));
     const double t_end = now_s();
     t->wall_s = t_end - t0;
-    float ms = 0;
-    HIPCK(hipEventElapsedTime(&ms, me.ev0, me.ev1));
-    t->device_s = ms * 1e-3;
-    t->launches = 1;
-    t->nwg = ll ? 1 : a.nwg;
-    t->protocol = ll ? kProtoLL : a.pull ? kProtoPull : kProtoBulk;
-    t->recv_done = __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE);
-    t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
-    // phases (mpx_last_phases): the kernel's own clock splits its span; the
-    // host's clock brackets it (launch before, completion after)
     const u64 te = __atomic_load_n(&me.status->t_entry, __ATOMIC_ACQUIRE);
     const u64 tp = __atomic_load_n(&me.status->t_posted, __ATOMIC_ACQUIRE);
     const u64 tx = __atomic_load_n(&me.status->t_exit, __ATOMIC_ACQUIRE);
+    const double kernel_s = (te && tx >= te) ? (double)(tx - te) * 1e-8 : 0;
+    if (armed) {
+        t->device_s = kernel_s;   // from go seen to the last workgroup's end (s_memrealtime)
+    } else {
+        float ms = 0;
+        HIPCK(hipEventElapsedTime(&ms, me.ev0, me.ev1));
+        t->device_s = ms * 1e-3;
+    }
+    t->launches = 1;
+    t->nwg = kc.ll ? 1 : a.nwg;
+    t->protocol = kc.ll ? kProtoLL : a.pull ? kProtoPull : kProtoBulk;
+    t->recv_done = __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE);
+    t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
+    // phases (mpx_last_phases): the kernel's own clock splits its span; the
+    // host's clock brackets it (launch or go before, completion after)
     mpx_phases& ph = me.phases;
     ph = mpx_phases{};
     ph.wall_s = t->wall_s;
-    ph.host_prep_s = t0 - t_call;
-    ph.kernel_s = (te && tx >= te) ? (double)(tx - te) * 1e-8 : 0;
+    ph.host_prep_s = armed ? 0 : t0 - t_call;
+    ph.kernel_s = kernel_s;
     ph.posted_wait_s = (te && tp >= te) ? (double)(tp - te) * 1e-8 : 0;
-    if (t_done > 0 && ph.kernel_s > 0) {
-        ph.launch_to_start_s = (t_done - t0) - ph.kernel_s;
+    if (t_done > 0 && kernel_s > 0) {
+        ph.launch_to_start_s = (t_done - t0) - kernel_s;
         ph.done_to_return_s = t_end - t_done;
     }
+    ph.armed = armed ? 1 : 0;
     const unsigned err = __atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE);
+    if (err == 2) {
+        me.broken = true;
+        return fail(MPX_ERR_TIMEOUT, "rank %d: the armed transfer was not started within its deadline", kc.my_rank);
+    }
     if (err) {
         me.broken = true;
         return fail(MPX_ERR_TIMEOUT, "rank %d <- rank %d: device wait timed out at iteration %u (mode %d, %lld B)",
-                    my_rank, peer_rank, me.status->where - 1, mode, len);
+                    kc.my_rank, kc.peer_rank, me.status->where - 1, kc.mode, kc.len);
     }
-    me.tx_seq[peer_rank] += (u64)iters;
-    me.rx_seq[peer_rank] += (u64)iters;
+    me.tx_seq[kc.peer_rank] += (u64)kc.iters;
+    me.rx_seq[kc.peer_rank] += (u64)kc.iters;
     return MPX_OK;
+}
+
+int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int group, int iters,
+               long long len, const mpx_xfer_opts* o, mpx_timing* t) {
+    const double t_call = now_s();
+    KernelCall kc;
+    TRY(prepare_call(ctx, me, peer, my_rank, peer_rank, mode, group, iters, len, o, &kc));
+    TRY(launch_call(me, kc, false));
+    return complete_call(me, kc, false, t_call, kc.t_launch, t);
+}
+
+// An armed call ends without a transfer: go = token | kGoCancel, wait for
+// the kernel, and the call number it took back (the peer never saw it: the
+// kernel exits before posting its receives).
+int disarm(Rank& me) {
+    if (!me.armed) return MPX_OK;
+    KernelCall& kc = *me.armed;
+    __atomic_store_n(&me.status->go, kc.a.go_token | kGoCancel, __ATOMIC_RELEASE);
+    double t_done = 0;
+    const int st = wait_kernel(me, kc.a.done_token, true, &t_done);
+    if (kc.iters > 0 && !test_knobs().no_posted) --me.calls[kc.peer_rank];
+    delete me.armed;
+    me.armed = nullptr;
+    return st;
 }
 
 // ---------------------------------------------------------------------------
@@ -1295,6 +1390,10 @@ int mpx_finalize(mpx_ctx* ctx) {
     std::vector<std::pair<int, hipStream_t>> ss;
     for (int i = 0; i < MPX_MAX_RANKS; ++i) {
         Rank& rk = ctx->r[i];
+        if (rk.armed) {                 // an armed call never started: cancel it
+            DeviceGuard g(rk.dev);
+            (void)disarm(rk);
+        }
         if (rk.comm) (void)ncclCommDestroy(rk.comm);
         rk.comm = nullptr;
         if (rk.local && rk.stream) ss.emplace_back(rk.dev, rk.stream);
@@ -1692,10 +1791,10 @@ int mpx_rank_import(mpx_ctx* ctx, int rank, const void* desc) {
     return MPX_OK;
 }
 
-int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, void* tx, void* rx,
-                int buff_len, const mpx_xfer_opts* opts, mpx_timing* t) {
-    if (!ctx || !t) return fail(MPX_ERR_INVALID, "NULL argument");
-    memset(t, 0, sizeof *t);
+namespace {
+// Argument checks and per-rank set-up shared by mpx_xfer_ex and mpx_xfer_arm.
+int check_call(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, void* tx, void* rx,
+               int buff_len, const mpx_xfer_opts* opts) {
     if (mode < MPX_MODE_PINGPONG || mode > MPX_MODE_UNIDIR) return fail(MPX_ERR_INVALID, "mode %d", mode);
     if (my_group != 0 && my_group != 1) return fail(MPX_ERR_INVALID, "group %d", my_group);
     if (my_rank < 0 || my_rank >= ctx->nranks || peer_rank < 0 || peer_rank >= ctx->nranks)
@@ -1732,6 +1831,101 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
         TRY(ensure_ring(me));
         TRY(ensure_ring(peer));
     }
+    return MPX_OK;
+}
+
+// After a completed loop: its algorithmic bytes and, in check mode, every
+// received payload's checksum against the peer's tx — in the non-blocking
+// loop too, where each receive has a slot of its own (k_xfer_nbcheck /
+// SdmaOps::nb_checked).
+int finish_xfer(Rank& me, int mode, int my_group, int my_rank, int iters, int buff_len, const mpx_xfer_opts* opts,
+                mpx_timing* t) {
+    t->bytes = (uint64_t)buff_len * (uint64_t)iters * (mode == MPX_MODE_UNIDIR ? 1u : 2u);
+    if (!(opts && opts->check) || iters <= 0) return MPX_OK;
+    DeviceGuard g(me.dev);
+    HIPCK(g.err);
+    std::vector<u64> raw((size_t)iters);
+    // the rank's own stream: a null-stream copy would wait for every
+    // blocking stream of the device, i.e. for other pairs' kernels
+    HIPCK(hipMemcpyAsync(raw.data(), me.csum, (size_t)iters * sizeof(u64), hipMemcpyDeviceToHost, me.stream));
+    HIPCK(hipStreamSynchronize(me.stream));
+    const bool ack = mode == MPX_MODE_UNIDIR && my_group == 1;
+    const u64 n = ack ? 1 : (u64)buff_len;   // the ack is always 1 byte (mpi_perf.c:137,142)
+    const u64 want = ack ? opts->expect_ack : opts->expect_checksum;
+    int bad = 0;
+    for (int i = 0; i < iters; ++i)
+        if ((raw[i] ^ mix64_host(n)) != want) ++bad;
+    t->check_failures = bad;
+    t->check_iters = (uint64_t)iters;
+    if (bad) return fail(MPX_ERR_CHECK, "rank %d: %d of %d received payloads failed the checksum", my_rank, bad, iters);
+    return MPX_OK;
+}
+
+// does an armed call match the arguments mpx_xfer_ex was given?
+bool armed_matches(const KernelCall& kc, int mode, int group, int peer_rank, int iters, long long len,
+                   const mpx_xfer_opts* o) {
+    return kc.mode == mode && kc.group == group && kc.peer_rank == peer_rank && kc.iters == iters && kc.len == len &&
+           kc.check == ((o && o->check) ? 1 : 0) && kc.flags == (o ? o->flags : 0) && kc.nwg_opt == (o ? o->nwg : 0) &&
+           kc.timeout_ms == (o ? o->timeout_ms : 0) && kc.expect == (o ? o->expect_checksum : 0) &&
+           kc.expect_ack == (o ? o->expect_ack : 0);
+}
+}  // namespace
+
+int mpx_xfer_arm(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, void* tx, void* rx,
+                 int buff_len, const mpx_xfer_opts* opts) {
+    if (!ctx) return fail(MPX_ERR_INVALID, "NULL argument");
+    TRY(check_call(ctx, mode, my_group, my_rank, peer_rank, iters, tx, rx, buff_len, opts));
+    if (ctx->engine != MPX_ENGINE_KERNEL) return MPX_OK;   // nothing to launch ahead (include/mpx.h)
+    Rank& me = ctx->r[my_rank];
+    Rank& peer = ctx->r[peer_rank];
+    if (me.armed) return fail(MPX_ERR_STATE, "rank %d is already armed (start or disarm it first)", my_rank);
+    DeviceGuard g(me.dev);
+    HIPCK(g.err);
+    KernelCall* kc = new KernelCall;
+    int st = prepare_call(ctx, me, peer, my_rank, peer_rank, mode, my_group, iters, buff_len, opts, kc);
+    if (st == MPX_OK) st = launch_call(me, *kc, true);
+    if (st != MPX_OK) {
+        delete kc;
+        return st;
+    }
+    me.armed = kc;
+    return MPX_OK;
+}
+
+int mpx_xfer_disarm(mpx_ctx* ctx, int my_rank) {
+    if (!ctx) return fail(MPX_ERR_INVALID, "NULL argument");
+    if (my_rank < 0 || my_rank >= ctx->nranks || !ctx->r[my_rank].local)
+        return fail(MPX_ERR_STATE, "rank %d is not a local rank", my_rank);
+    Rank& me = ctx->r[my_rank];
+    DeviceGuard g(me.dev);
+    HIPCK(g.err);
+    return disarm(me);
+}
+
+int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, void* tx, void* rx,
+                int buff_len, const mpx_xfer_opts* opts, mpx_timing* t) {
+    if (!ctx || !t) return fail(MPX_ERR_INVALID, "NULL argument");
+    memset(t, 0, sizeof *t);
+    const double t_call = now_s();
+    TRY(check_call(ctx, mode, my_group, my_rank, peer_rank, iters, tx, rx, buff_len, opts));
+    Rank& me = ctx->r[my_rank];
+    Rank& peer = ctx->r[peer_rank];
+    const bool pull = ctx->engine != MPX_ENGINE_RCCL && pull_requested(opts);
+    if (me.armed) {
+        // start the armed call: one host store; the kernel has been waiting for it
+        KernelCall& kc = *me.armed;
+        if (!armed_matches(kc, mode, my_group, peer_rank, iters, buff_len, opts))
+            return fail(MPX_ERR_STATE, "rank %d is armed for another call (disarm it first)", my_rank);
+        DeviceGuard g(me.dev);
+        HIPCK(g.err);
+        const double t0 = now_s();
+        __atomic_store_n(&me.status->go, kc.a.go_token, __ATOMIC_RELEASE);
+        const int st = complete_call(me, kc, true, t_call, t0, t);
+        delete me.armed;
+        me.armed = nullptr;
+        if (st != MPX_OK) return st;
+        return finish_xfer(me, mode, my_group, my_rank, iters, buff_len, opts, t);
+    }
     DeviceGuard g(me.dev);
     HIPCK(g.err);
     int st;
@@ -1746,26 +1940,7 @@ int mpx_xfer_ex(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank
         default: st = run_rccl(me, peer, my_rank, peer_rank, mode, my_group, iters, buff_len, opts, t); break;
     }
     if (st != MPX_OK) return st;
-    t->bytes = (uint64_t)buff_len * (uint64_t)iters * (mode == MPX_MODE_UNIDIR ? 1u : 2u);
-    // every received payload — in the non-blocking loop too, where each
-    // receive has a slot of its own (k_xfer_nbcheck / SdmaOps::nb_checked)
-    if (check && iters > 0) {
-        std::vector<u64> raw((size_t)iters);
-        // the rank's own stream: a null-stream copy would wait for every
-        // blocking stream of the device, i.e. for other pairs' kernels
-        HIPCK(hipMemcpyAsync(raw.data(), me.csum, (size_t)iters * sizeof(u64), hipMemcpyDeviceToHost, me.stream));
-        HIPCK(hipStreamSynchronize(me.stream));
-        const bool ack = mode == MPX_MODE_UNIDIR && my_group == 1;
-        const u64 n = ack ? 1 : (u64)buff_len;   // the ack is always 1 byte (mpi_perf.c:137,142)
-        const u64 want = ack ? opts->expect_ack : opts->expect_checksum;
-        int bad = 0;
-        for (int i = 0; i < iters; ++i)
-            if ((raw[i] ^ mix64_host(n)) != want) ++bad;
-        t->check_failures = bad;
-        t->check_iters = (uint64_t)iters;
-        if (bad) return fail(MPX_ERR_CHECK, "rank %d: %d of %d received payloads failed the checksum", my_rank, bad, iters);
-    }
-    return MPX_OK;
+    return finish_xfer(me, mode, my_group, my_rank, iters, buff_len, opts, t);
 }
 
 namespace {

@@ -72,10 +72,10 @@ class XferOpts(C.Structure):
 
 class Phases(C.Structure):
     _fields_ = [(k, C.c_double) for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",
-                                           "done_to_return_s")]
+                                           "done_to_return_s")] + [("armed", C.c_int32), ("reserved", C.c_int32)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
 def pattern_key(seed: int, src: int, dst: int, it: int) -> int:
@@ -109,6 +109,9 @@ _SIGS = {
                               C.c_int, C.POINTER(XferOpts), C.POINTER(Timing)]),
     "mpx_xfer_prepare": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.POINTER(XferOpts)]),
+    "mpx_xfer_arm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                               C.c_int, C.POINTER(XferOpts)]),
+    "mpx_xfer_disarm": (C.c_int, [C.c_void_p, C.c_int]),
     "mpx_barrier": (C.c_int, [C.c_void_p, C.c_int]),
     "mpx_rccl_version": (C.c_int, [C.POINTER(C.c_int), C.c_char_p, C.c_int]),
     "mpx_rccl_get_unique_id": (C.c_int, [C.c_void_p]),
@@ -260,6 +263,20 @@ class Context:
                                 C.c_void_p(rx.ptr), length, C.byref(o), C.byref(t))
         check(st, "mpx_xfer_ex")
         return t
+
+    def arm(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, tx: Buffer, rx: Buffer,
+            length: int, check_payload: bool = False, expect: int = 0, expect_ack: int = 0, timeout_ms: int = 0,
+            nwg: int = 0, stream: bool = False, pull: bool = False, stage: bool = True) -> None:
+        """mpx_xfer_arm: launch the next xfer with these arguments now; the
+        xfer call with the same arguments starts it (kernel engine)"""
+        flags = (XFER_STREAM if stream else 0) | (XFER_PULL if pull else 0) | (0 if stage else XFER_NOSTAGE)
+        o = XferOpts(check=1 if check_payload else 0, flags=flags, expect_checksum=expect,
+                     expect_ack=expect_ack, timeout_ms=timeout_ms, nwg=nwg)
+        check(self.L.mpx_xfer_arm(self.h, mode, group, my_rank, peer_rank, iters, C.c_void_p(tx.ptr),
+                                  C.c_void_p(rx.ptr), length, C.byref(o)), "mpx_xfer_arm")
+
+    def disarm(self, rank: int) -> None:
+        check(self.L.mpx_xfer_disarm(self.h, rank), "mpx_xfer_disarm")
 
     def prepare(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, length: int,
                 timeout_ms: int = 0, pull: bool = False) -> None:

@@ -55,6 +55,10 @@ class FakeMpx:
         return "0000:00:00.0" if scenario in ("one_gpu", "rccl_one_gpu") else f"0000:{rank + 1:02x}:00.0"
 
     @staticmethod
+    def shutdown():
+        FakeMpx.log.append(["shutdown"])
+
+    @staticmethod
     def rccl_version():
         return {"version": 22707, "release": "2.27.7", "library": "fake"}
 
@@ -115,6 +119,13 @@ class FakeMpx:
                                                                                        else 0.5)
                 return Timing(ms * 1e-3, ms * 1e-3)
             return Timing(0.002, 0.001 * (1 + me))
+
+        def arm(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,
+                timeout_ms=0, nwg=0, stream=False, pull=False, stage=True):
+            FakeMpx.log.append(["arm", self.engine, mode, group, me, peer, iters, n])
+
+        def disarm(self, r):
+            FakeMpx.log.append(["disarm", self.engine, r])
 
         def phases(self, r):
             return {k: 1e-6 for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",

@@ -61,18 +61,29 @@ class Pairs:
         tx = self.bufs[self.peer(r)][0]
         return self.c.checksum(tx, n), self.c.checksum(tx, 1)
 
-    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0, stream=False, pull=False):
+    def run(self, mode, n, iters, check=True, timeout_ms=10000, ranks=None, nwg=0, stream=False, pull=False,
+            armed=False):
+        """every rank's side on a thread of its own; armed: each side arms
+        its call (mpx_xfer_arm), all sides meet at a barrier (the hosts'
+        mpi_perf.c:499), then start it"""
         ranks = list(range(2 * self.np)) if ranks is None else ranks
         exp = {r: self.expect(r, n) for r in ranks}
         out, errs = {}, {}
+        bar = threading.Barrier(len(ranks))
 
         def side(r):
+            kw = dict(check_payload=check, expect=exp[r][0], expect_ack=exp[r][1], timeout_ms=timeout_ms, nwg=nwg,
+                      stream=stream, pull=pull)
+            args = (mode, self.group(r), r, self.peer(r), iters, self.bufs[r][0], self.bufs[r][1], n)
             try:
-                out[r] = self.c.xfer(mode, self.group(r), r, self.peer(r), iters, self.bufs[r][0], self.bufs[r][1],
-                                     n, check_payload=check, expect=exp[r][0], expect_ack=exp[r][1],
-                                     timeout_ms=timeout_ms, nwg=nwg, stream=stream, pull=pull)
+                if armed:
+                    self.c.arm(*args, **kw)
+                    bar.wait()
+                out[r] = self.c.xfer(*args, **kw)
             except mpx.MpxError as e:
                 errs[r] = e
+                if armed:
+                    bar.abort()
 
         th = [threading.Thread(target=side, args=(r,)) for r in ranks]
         for t in th:

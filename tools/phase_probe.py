@@ -6,7 +6,10 @@ shape; per call and side, mpx_last_phases splits the wall time into host
 preparation, launch -> kernel start, the wait for the peer's receives, the
 kernel and completion -> return.  Medians over the calls.
 
-    MPX_SYNC=query|event python tools/phase_probe.py [calls]
+    MPX_SYNC=query|event python tools/phase_probe.py [calls] [armed]
+
+armed: every call is armed (mpx_xfer_arm) before the barrier and started
+after it, so its launch is outside the timed call.
 """
 import json
 import os
@@ -19,6 +22,7 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 import mpx  # noqa: E402
 
 CALLS = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+ARMED = "armed" in sys.argv[2:]
 SHAPES = [("unidir", mpx.MODE_UNIDIR, 456131, 10), ("unidir", mpx.MODE_UNIDIR, 4 << 20, 10),
           ("pingpong", mpx.MODE_PINGPONG, 8, 10), ("unidir", mpx.MODE_UNIDIR, 4 << 20, 500)]
 CAP = 4 << 20
@@ -38,6 +42,8 @@ with mpx.Context(2, "kernel") as c:
         def side(r):
             try:
                 for k in range(CALLS + 2):
+                    if ARMED:
+                        c.arm(mode, 1 - r, r, 1 - r, iters, bufs[r][0], bufs[r][1], n)
                     bar.wait()
                     t = c.xfer(mode, 1 - r, r, 1 - r, iters, bufs[r][0], bufs[r][1], n)
                     if k >= 2:
@@ -50,14 +56,15 @@ with mpx.Context(2, "kernel") as c:
             x.start()
         for x in th:
             x.join()
-        rec = dict(sync=os.environ.get("MPX_SYNC", "query"), shape=name, bytes=n, iters=iters, calls=CALLS)
+        rec = dict(sync=os.environ.get("MPX_SYNC", "query"), armed=ARMED, shape=name, bytes=n, iters=iters, calls=CALLS)
         if errs:
             rec["error"] = errs[:2]
         else:
             walls = [max(a["wall_s"], b["wall_s"]) for a, b in zip(rows[0], rows[1])]
             rec["pair_wall_us_median"] = round(statistics.median(walls) * 1e6, 2)
             for r, label in ((0, "g1"), (1, "g0")):
-                rec[label] = {k: round(statistics.median(x[k] for x in rows[r]) * 1e6, 2) for k in rows[r][0]}
+                rec[label] = {k: round(statistics.median(x[k] for x in rows[r]) * 1e6, 2) for k in rows[r][0]
+                              if k != "armed"}
             if mode == mpx.MODE_UNIDIR:
                 rec["GBps"] = round(n * iters / statistics.median(walls) / 1e9, 2)
         print(json.dumps(rec), flush=True)
