@@ -28,6 +28,7 @@ void mpxh_defaults(mpxh_options *o)
     o->num_runs = 1;                /* :392 */
     o->engine = 0;
     o->timeout_ms = 10000;
+    o->arm = 1;
 }
 
 int mpxh_engine_from_name(const char *s)
@@ -64,7 +65,8 @@ void mpxh_print_usage(FILE *f)
 		    -a <all-pairs circle-method rounds 0|1>\n\
 		    -c <checksum every payload 0|1|2 (2: seeded-pattern payloads)>\n\
 		    -S <min:max power-of-two message-size sweep>\n\
-		    -t <device wait timeout ms>\n");
+		    -t <device wait timeout ms>\n\
+		    -A <launch each run's kernel before the barrier 0|1 (default 1)>\n");
 }
 
 /* parse_args, mpi_perf.c:273-339 */
@@ -73,7 +75,7 @@ int mpxh_parse_args(mpxh_options *o, int argc, char **argv)
     int opt;
     optind = 1;
     opterr = 0;
-    while ((opt = getopt(argc, argv, ":f:n:d:p:i:b:u:h:r:l:x:w:e:a:c:S:t:g:")) != -1) {
+    while ((opt = getopt(argc, argv, ":f:n:d:p:i:b:u:h:r:l:x:w:e:a:c:S:t:g:A:")) != -1) {
         switch (opt) {
         case 'f': strncpy(o->group1_hostfile, optarg, MPXH_MAX_HOST - 1); break;
         case 'n': o->group_size = atoi(optarg); break;
@@ -102,6 +104,7 @@ int mpxh_parse_args(mpxh_options *o, int argc, char **argv)
         }
         case 't': o->timeout_ms = atoi(optarg); break;
         case 'g': strncpy(o->gpus, optarg, sizeof o->gpus - 1); break;
+        case 'A': o->arm = atoi(optarg); break;
         default: return MPXH_PARSE_USAGE; /* includes -h and a missing value */
         }
     }
@@ -397,6 +400,7 @@ int mpxh_parse_args_windows(mpxh_options *o, int argc, char **argv)
         o->sweep_min = x.sweep_min;
         o->sweep_max = x.sweep_max;
         o->timeout_ms = x.timeout_ms;
+        o->arm = x.arm;
         memcpy(o->gpus, x.gpus, sizeof o->gpus);
     }
     mpxh_uuid_windows(o->uuid); /* :196 */

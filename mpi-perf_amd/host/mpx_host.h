@@ -41,6 +41,8 @@ typedef struct mpxh_options {
     int sweep_min, sweep_max;       /* -S  min:max  power-of-two size sweep   */
     int timeout_ms;                 /* -t  per-wait device timeout            */
     char gpus[256];                 /* -g  rank->GPU list "0,1,..."          */
+    int arm;                        /* -A  1 (default) = arm each run's kernel
+                                           before the barrier (mpx_xfer_arm) */
 } mpxh_options;
 
 /* parse status */
@@ -55,7 +57,7 @@ enum {
 /* defaults of main(), mpi_perf.c:388-392 (+ the new fields) */
 void mpxh_defaults(mpxh_options *o);
 /* parse_args, mpi_perf.c:273-339 (getopt ":f:n:d:p:i:b:u:h:r:l:x:" plus
-   "w:e:a:c:S:t:g:"); fills o->uuid with a fresh v4 UUID.  Resets getopt. */
+   "w:e:a:c:S:t:g:A:"); fills o->uuid with a fresh v4 UUID.  Resets getopt. */
 int mpxh_parse_args(mpxh_options *o, int argc, char **argv);
 /* print_usage, mpi_perf.c:20-32 (the reference's text, then the new flags) */
 void mpxh_print_usage(FILE *f);

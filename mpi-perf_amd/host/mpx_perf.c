@@ -203,8 +203,22 @@ static void open_logs(int rank, rank_files *f)
     if (f->gpu_fp)
         fprintf(f->gpu_fp, "Timestamp,JobId,Rank,Engine,Mode,Device,PeerRank,PeerDevice,BufferSize,NumOfBuffers,"
                            "WallTimems,DeviceTimems,GBps,Protocol,Workgroups,CheckedPayloads,CheckFailures,RunId,RecvDone,"
-                           "RecvDigest\n");
+                           "RecvDigest,Launch,Rccl\n");
     f->t_last_logtime = wtime();
+}
+
+/* the RCCL this process runs, "<release>:<library path>" (engine rccl), for
+   the gpu-*.csv side file: bench.py, which loads torch first, runs torch's
+   bundled RCCL; mpx_perf the image's */
+static char rccl_build[600];
+
+static void note_rccl_build(void)
+{
+    int v = 0;
+    char path[512] = {0};
+    if (opt.engine != MPX_ENGINE_RCCL || mpx_rccl_version(&v, path, sizeof path) != MPX_OK) return;
+    snprintf(rccl_build, sizeof rccl_build, "%d.%d.%d:%s", v / 10000, v / 100 % 100, v % 100, path);
+    fprintf(stderr, "[mpx_perf] RCCL %s\n", rccl_build);
 }
 
 static int xfer_mode(void)
@@ -260,6 +274,11 @@ static void *rank_main(void *arg)
                inside the timed call (the reference's timer brackets only the
                loop, mpi_perf.c:501-533) */
             if (!opt.use_dotnet) MPX_CHECK(mpx_xfer_prepare(ctx, xfer_mode(), group, r, peer, opt.iters, B, &xo));
+            /* -A 1: the run's kernel is launched now and started by the
+               mpx_xfer_ex after the barrier (MPI_Start of a persistent
+               request), so the launch is not inside the timed loop */
+            if (!opt.use_dotnet && opt.arm)
+                MPX_CHECK(mpx_xfer_arm(ctx, xfer_mode(), group, r, peer, opt.iters, tx_of[r], rx_of[r], B, &xo));
             barrier(); /* MPI_Barrier, mpi_perf.c:499 */
             const double t_start = wtime();
             mpx_timing tm;
@@ -289,12 +308,13 @@ static void *rank_main(void *arg)
                     const double gbps = my_time > 0 ? (double)tm.bytes / my_time / 1e9 : 0.0;
                     static const char *proto[] = {"ll", "bulk", "sdma", "rccl", "copy", "copy_steps", "copy_pipe", "pull",
                                                  "sdma_pull"};
-                    fprintf(files.gpu_fp, "%s,%s,%d,%s,%d,%d,%d,%d,%d,%d,%.4f,%.4f,%.3f,%s,%d,%llu,%d,%lld,%llu,%llu\n", ts,
+                    fprintf(files.gpu_fp, "%s,%s,%d,%s,%d,%d,%d,%d,%d,%d,%.4f,%.4f,%.3f,%s,%d,%llu,%d,%lld,%llu,%llu,%s,%s\n", ts,
                             opt.uuid, r, mpxh_engine_name(opt.engine), xfer_mode(), dev_of[r], peer, dev_of[peer], B,
                             opt.iters, my_time * 1e3, tm.device_s * 1e3, gbps,
                             (tm.protocol >= 0 && tm.protocol <= 8) ? proto[tm.protocol] : "?", tm.nwg,
                             (unsigned long long)tm.check_iters, tm.check_failures, run_idx,
-                            (unsigned long long)tm.recv_done, (unsigned long long)tm.recv_digest);
+                            (unsigned long long)tm.recv_done, (unsigned long long)tm.recv_digest,
+                            (opt.arm && opt.engine == MPX_ENGINE_KERNEL) ? "armed" : "inline", rccl_build);
                 }
             }
 
@@ -399,6 +419,7 @@ static void connect_ranks(void)
         if (me == 0) MPX_CHECK(mpx_rccl_get_unique_id(id));
         if (mpxb_bcast0(boot, id, sizeof id) != 0) boot_failed();
         MPX_CHECK(mpx_rccl_init_rank(ctx, me, world, id));
+        note_rccl_build();
         return;
     }
     static unsigned char all[MPXH_MAX_RANKS][MPX_RANK_DESC_BYTES];
@@ -677,8 +698,10 @@ int main(int argc, char **argv)
         }
         if (procs)
             connect_ranks();
-        else if (opt.engine == MPX_ENGINE_RCCL)
+        else if (opt.engine == MPX_ENGINE_RCCL) {
             MPX_CHECK(mpx_rccl_init_all(ctx));
+            note_rccl_build();
+        }
     }
 
     if (procs) {
@@ -686,6 +709,7 @@ int main(int argc, char **argv)
         rank_main((void *)(intptr_t)me);
         barrier(); /* MPI_Barrier, mpi_perf.c:579: no peer still maps our buffers */
         if (ctx) MPX_CHECK(mpx_finalize(ctx)); /* frees tx/rx too */
+        if (ctx) MPX_CHECK(mpx_shutdown()); /* pooled rank streams, before exit's teardown */
         barrier();
         mpxb_finalize(boot);
         return 0;
@@ -704,5 +728,10 @@ int main(int argc, char **argv)
         }
     }
     if (ctx) MPX_CHECK(mpx_finalize(ctx));
+    /* the pooled rank streams go before exit: left to the HIP runtime's exit
+       teardown, a profiler tool's exit-time finalizer (rocprofiler-sdk, as
+       under rocprofv3 --pmc) faulted in libhsa-runtime64
+       (profiles/r04_exit_segv_stack.txt) */
+    if (ctx) MPX_CHECK(mpx_shutdown());
     return 0;
 }

@@ -26,6 +26,20 @@ def test_every_header_symbol_is_exported():
         assert f" T {s}\n" in dyn or f" T {s}" in dyn, s
 
 
+def test_counter_library_exports_its_header():
+    """libmpxprof.so (bench.py's in-process counters) exports every function
+    include/mpxprof.h declares; loading it starts nothing (no HIP here)."""
+    from mpx import counters
+    hdr = os.path.join(os.path.dirname(mpx.HEADER_PATH), "mpxprof.h")
+    import re
+    txt = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+    names = sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_]+\s*\*?\s*(mpxprof_[a-z_]+)\s*\(", txt, flags=re.M)))
+    assert names == ["mpxprof_begin", "mpxprof_end", "mpxprof_error", "mpxprof_ready", "mpxprof_register"]
+    dyn = subprocess.run(["nm", "-D", "--defined-only", counters.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert f" T {n}" in dyn, n
+
+
 def test_version_and_strerror():
     L = mpx.lib()
     # 2: recv_done / recv_digest; 3: 64 ranks per context; 4: receive-posted mailbox word;
