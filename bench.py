@@ -1023,6 +1023,53 @@ def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iter
     return res, engine_used
 
 
+class SpinBarrierDist:
+    """torch.distributed as the pairs path uses it, with barrier() replaced
+    by the node-local spin barrier (mpx/spin.py): the barrier in front of
+    every timed loop (mpi_perf.c:499) then lets the ranks leave within about
+    a microsecond, as MPI's intra-node barrier does, instead of a gloo TCP
+    round trip apart.  Collectives that carry data stay gloo's."""
+
+    def __init__(self, dist, spin):
+        self._dist, self._spin = dist, spin
+
+    def barrier(self):
+        self._spin.wait()
+
+    def __getattr__(self, k):
+        return getattr(self._dist, k)
+
+
+def spin_barrier_dist(dist, rank: int, world: int):
+    """(SpinBarrierDist, spin) when every rank opened the shm barrier, else
+    (dist, None): every rank decides alike."""
+    from mpx import spin as sp
+    name = f"/mpxbar-bench-{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}"
+    s, err = None, ""
+    try:
+        if rank == 0:
+            sp.unlink(name)                       # a stale one from a killed run
+            s = sp.SpinBarrier(name, world, True)
+    except Exception as e:  # noqa: BLE001
+        err = str(e)
+    dist.barrier()
+    try:
+        if rank != 0:
+            s = sp.SpinBarrier(name, world, False)
+    except Exception as e:  # noqa: BLE001
+        err = str(e)
+    flags = [None] * world
+    dist.all_gather_object(flags, err)
+    if rank == 0:
+        sp.unlink(name)                           # every rank has it mapped (or gave up)
+    if any(flags):
+        print(f"[bench] spin barrier unavailable, gloo barriers: {[f for f in flags if f][0]}", file=sys.stderr)
+        if s is not None:
+            s.close()
+        return dist, None
+    return SpinBarrierDist(dist, s), s
+
+
 def quiet_stdout() -> int:
     """Route fd 1 to stderr for the rest of the run and return a duplicate
     of the real stdout: libraries print banners there (RCCL's version block
@@ -1120,6 +1167,9 @@ def main() -> None:
             dist.barrier()
         torch.cuda.synchronize()
 
+    # N > 1: the per-round barriers of the pairs path spin in shared memory
+    pdist, spin = (spin_barrier_dist(dist, rank, world) if dist is not None else (None, None))
+
     extras = {}
     if one:
         workload = "local_d2d_copy"
@@ -1187,7 +1237,7 @@ def main() -> None:
         metric_unit = "GB/s"
         # --no-extras: nothing after the timed steps (profiling runs select
         # the timed launches as the last ones)
-        res, engine_used = pairs_with_fallback(mpx, torch, dist, args.engine, rank, world, dev, nbytes, iters,
+        res, engine_used = pairs_with_fallback(mpx, torch, pdist, args.engine, rank, world, dev, nbytes, iters,
                                                args.steps, args.warmup, barrier_sync, extras,
                                                latency=not args.no_extras, prof=prof)
         elapsed, total = res["elapsed"], res["total"]
@@ -1217,6 +1267,10 @@ def main() -> None:
                       rounds=world - 1, pairs_per_round=world // 2, parallelism=f"pairs{world // 2}",
                       validated_rounds=res["validated_rounds"], push=res.get("push", "default"),
                       push_nwg=nwg_used,
+                      barrier=("node-local spin barrier in shared memory before every loop (mpx/spin.py)"
+                               if spin is not None else "gloo"),
+                      launch=("armed: each loop's kernel launched before its barrier, started by a host-memory "
+                              "word after it (mpx_xfer_arm)" if engine_used == "kernel" else "inline"),
                       # bytes of tx each pushing workgroup holds in LDS (read once per call; 0 = tx read from HBM)
                       stage=chunk if (engine_used == "kernel" and 0 < chunk <= 60 << 10) else 0)
         if "ll_max" in res:
@@ -1323,7 +1377,7 @@ def main() -> None:
             # (drain, flag, 1-byte ack) is then ~0.5 % of a push, so this is
             # the link rate the kernel engine reaches with B out of the
             # picture, the reference point for the 4 MiB headline's fraction
-            r3 = pairs_bench(mpx, torch, dist, "kernel", rank, world, dev, CEILING_BYTES, CEILING_ITERS, world - 1, 1,
+            r3 = pairs_bench(mpx, torch, pdist, "kernel", rank, world, dev, CEILING_BYTES, CEILING_ITERS, world - 1, 1,
                              barrier_sync, latency=False, tune=False)
             if r3.get("error"):
                 extras["unidir_64MiB_per_pair_GBps"] = r3["error"]
@@ -1343,9 +1397,9 @@ def main() -> None:
             if not pull and config["engine"].startswith(eng):
                 continue
             # 512 iterations: two graph-replayed SDMA chunks (run_sdma), no host-bound tail
-            r2 = pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
+            r2 = pairs_bench(mpx, torch, pdist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
                              latency=False, tune=False, pull=pull) if pull else \
-                pairs_bench(mpx, torch, dist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
+                pairs_bench(mpx, torch, pdist, eng, rank, world, dev, nbytes, 512, world - 1, 1, barrier_sync,
                             latency=False)
             # every round's payloads checksummed on this engine before timing
             # it (BASELINE config 5); pull: the engine's MPX_XFER_PULL form
@@ -1360,6 +1414,8 @@ def main() -> None:
         emit(out_fd, line)
     if dist is not None:
         dist.barrier()
+        if spin is not None:
+            spin.close()
         dist.destroy_process_group()
     # every context is finalized: the pooled rank streams go now, while the
     # process is whole — left to the exit teardown, they made the counter

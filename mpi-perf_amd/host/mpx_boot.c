@@ -21,7 +21,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -293,4 +297,109 @@ int mpxb_allreduce_f64(mpxb *b, double v, double *mn, double *mx, double *sum)
     if (mx) *mx = hi;
     if (sum) *sum = s;
     return 0;
+}
+
+/* ---- spin barrier ---------------------------------------------------------
+ * A central counter + generation word (each on its own cache line); the
+ * last arriver resets the counter and bumps the generation, everyone else
+ * spins on the generation.  In a process (threads mode) or in a POSIX shm
+ * object shared by the ranks of one node. */
+struct spin_words {
+    _Alignas(64) uint64_t count;
+    _Alignas(64) uint64_t gen;
+    _Alignas(64) int32_t n;
+};
+
+struct mpxb_spin {
+    struct spin_words *w;
+    int n;
+    int shared;
+    char name[128];
+};
+
+static double spin_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+int mpxb_spin_open(mpxb_spin **out, const char *name, int nranks, int create)
+{
+    *out = NULL;
+    if (nranks < 1) return err("spin barrier of %d ranks", nranks);
+    mpxb_spin *s = calloc(1, sizeof *s);
+    if (!s) return err("out of memory");
+    s->n = nranks;
+    if (!name) {
+        s->w = aligned_alloc(64, sizeof *s->w);
+        if (!s->w) {
+            free(s);
+            return err("out of memory");
+        }
+        memset(s->w, 0, sizeof *s->w);
+        s->w->n = nranks;
+        *out = s;
+        return 0;
+    }
+    snprintf(s->name, sizeof s->name, "%s", name);
+    const int fd = shm_open(name, create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+    if (fd < 0) {
+        free(s);
+        return err("shm_open(%s): %s", name, strerror(errno));
+    }
+    if (create && ftruncate(fd, (off_t)sizeof(struct spin_words)) != 0) {
+        close(fd);
+        shm_unlink(name);
+        free(s);
+        return err("ftruncate(%s): %s", name, strerror(errno));
+    }
+    void *p = mmap(NULL, sizeof(struct spin_words), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        if (create) shm_unlink(name);
+        free(s);
+        return err("mmap(%s): %s", name, strerror(errno));
+    }
+    s->w = p;
+    s->shared = 1;
+    if (create) __atomic_store_n(&s->w->n, nranks, __ATOMIC_RELEASE);   /* (ftruncate zeroed the words) */
+    else if (__atomic_load_n(&s->w->n, __ATOMIC_ACQUIRE) != nranks) {
+        mpxb_spin_close(s, 0);
+        return err("spin barrier %s: made for %d ranks, not %d", name, s->w ? s->w->n : -1, nranks);
+    }
+    *out = s;
+    return 0;
+}
+
+int mpxb_spin_wait(mpxb_spin *s, double timeout_s)
+{
+    struct spin_words *w = s->w;
+    const uint64_t g = __atomic_load_n(&w->gen, __ATOMIC_ACQUIRE);
+    if (__atomic_add_fetch(&w->count, 1, __ATOMIC_ACQ_REL) == (uint64_t)s->n) {
+        __atomic_store_n(&w->count, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&w->gen, g + 1, __ATOMIC_RELEASE);
+        return 0;
+    }
+    const double deadline = spin_now() + timeout_s;
+    for (unsigned long k = 1; __atomic_load_n(&w->gen, __ATOMIC_ACQUIRE) == g; ++k) {
+        __builtin_ia32_pause();
+        if ((k & 4095) == 0) {
+            if (spin_now() > deadline) return err("spin barrier: timed out after %.0f s", timeout_s);
+            if (k > (1ul << 20)) sched_yield();   /* a long wait (a slow rank): give the core back now and then */
+        }
+    }
+    return 0;
+}
+
+void mpxb_spin_close(mpxb_spin *s, int unlink_it)
+{
+    if (!s) return;
+    if (s->shared) {
+        munmap(s->w, sizeof(struct spin_words));
+        if (unlink_it) shm_unlink(s->name);
+    } else {
+        free(s->w);
+    }
+    free(s);
 }

@@ -49,6 +49,19 @@ int mpxb_barrier(mpxb *b);
  * rank gets bit-identical results (reduced in rank order) */
 int mpxb_allreduce_f64(mpxb *b, double v, double *mn, double *mx, double *sum);
 
+/* Spin barrier for the barrier in front of every timed loop (MPI_Barrier,
+ * mpi_perf.c:499): a TCP star round trip or a futex wake-up lets ranks leave
+ * tens of microseconds apart, and a rank's timer starts at its own exit, so
+ * that skew lands in short loops' records; MPI's intra-node barrier spins on
+ * shared memory.  name = NULL: in this process (threads); else a POSIX shm
+ * object (e.g. "/mpxbar-<job>") the ranks of one node share, created by one
+ * of them (create = 1) before the others open it.  Every wait is bounded by
+ * timeout_s.  Returns 0 or -1 (mpxb_error). */
+typedef struct mpxb_spin mpxb_spin;
+int mpxb_spin_open(mpxb_spin **out, const char *name, int nranks, int create);
+int mpxb_spin_wait(mpxb_spin *s, double timeout_s);
+void mpxb_spin_close(mpxb_spin *s, int unlink_it);
+
 const char *mpxb_error(void);
 
 #endif

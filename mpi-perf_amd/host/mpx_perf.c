@@ -43,6 +43,7 @@
 #include <errno.h>
 #include <execinfo.h>
 #include <pthread.h>
+#include <sys/mman.h>
 #include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -140,6 +141,39 @@ static void barrier(void)
     } else {
         pthread_barrier_wait(&bar);
     }
+}
+
+/* The barrier right in front of every timed loop (mpi_perf.c:499): a spin
+   barrier (threads: in this process; processes on one node: POSIX shared
+   memory named after the job id), so the ranks leave it within about a
+   microsecond as MPI's intra-node barrier lets them — a TCP round trip or a
+   futex wake-up let them leave tens of microseconds apart, and each rank's
+   timer starts at its own exit.  Ranks on several hosts use barrier(). */
+static mpxb_spin *start_bar;
+
+static void open_start_barrier(void)
+{
+    if (!procs) {
+        if (mpxb_spin_open(&start_bar, NULL, world, 1) != 0) boot_failed();
+        return;
+    }
+    if (multi_host) return;
+    char name[128];
+    snprintf(name, sizeof name, "/mpxbar-%s", opt.uuid);
+    if (me == 0 && mpxb_spin_open(&start_bar, name, world, 1) != 0) boot_failed();
+    barrier();
+    if (me != 0 && mpxb_spin_open(&start_bar, name, world, 0) != 0) boot_failed();
+    barrier();
+    if (me == 0) shm_unlink(name);   /* every rank has it mapped: the name can go now */
+}
+
+static void start_barrier(void)
+{
+    if (!start_bar) {
+        barrier();
+        return;
+    }
+    if (mpxb_spin_wait(start_bar, 600.0) != 0) boot_failed();
 }
 
 /* every rank learns every rank's tx checksums (check mode's expected values) */
@@ -279,7 +313,7 @@ static void *rank_main(void *arg)
                request), so the launch is not inside the timed loop */
             if (!opt.use_dotnet && opt.arm)
                 MPX_CHECK(mpx_xfer_arm(ctx, xfer_mode(), group, r, peer, opt.iters, tx_of[r], rx_of[r], B, &xo));
-            barrier(); /* MPI_Barrier, mpi_perf.c:499 */
+            start_barrier(); /* MPI_Barrier, mpi_perf.c:499 */
             const double t_start = wtime();
             mpx_timing tm;
             memset(&tm, 0, sizeof tm);
@@ -705,21 +739,25 @@ int main(int argc, char **argv)
     }
 
     if (procs) {
+        open_start_barrier();
         barrier();
         rank_main((void *)(intptr_t)me);
         barrier(); /* MPI_Barrier, mpi_perf.c:579: no peer still maps our buffers */
         if (ctx) MPX_CHECK(mpx_finalize(ctx)); /* frees tx/rx too */
         if (ctx) MPX_CHECK(mpx_shutdown()); /* pooled rank streams, before exit's teardown */
         barrier();
+        mpxb_spin_close(start_bar, 0);
         mpxb_finalize(boot);
         return 0;
     }
 
     pthread_barrier_init(&bar, NULL, (unsigned)world);
+    open_start_barrier();
     pthread_t th[MPXH_MAX_RANKS];
     for (int r = 0; r < world; ++r) pthread_create(&th[r], NULL, rank_main, (void *)(intptr_t)r);
     for (int r = 0; r < world; ++r) pthread_join(th[r], NULL);
     pthread_barrier_destroy(&bar);
+    mpxb_spin_close(start_bar, 0);
 
     if (!opt.use_dotnet) {
         for (int r = 0; r < world; ++r) {

@@ -195,7 +195,10 @@ if __name__ == "__main__":
                                              dist.barrier, latency=False))
         else:
             prof = FakeProf if scenario in ("counters", "one_gpu") else None
-            res, used = bench.pairs_with_fallback(FakeMpx, torch, dist, "kernel", rank, world, 0, nbytes, 7, 5, 2,
+            # the per-round barriers spin in shared memory, as in bench.main (world 2 and 4 here)
+            d, spin = bench.spin_barrier_dist(dist, rank, world) if scenario == "ok" else (dist, None)
+            out["spin"] = spin is not None
+            res, used = bench.pairs_with_fallback(FakeMpx, torch, d, "kernel", rank, world, 0, nbytes, 7, 5, 2,
                                                   dist.barrier, extras, prof=prof)
             out.update(res=res, engine_used=used, extras=extras, passes=FakeProf.passes)
     except SystemExit as e:

@@ -20,6 +20,9 @@ import bench_dist_worker as W  # noqa: E402
 
 W.rank = int(os.environ["RANK"])
 W.scenario = sys.argv[1]
+from mpx import spin as _spin  # noqa: E402  (the real node-local spin barrier: host code, no GPU)
+
+W.FakeMpx.spin = _spin
 sys.modules["mpx"] = W.FakeMpx          # bench.main's `import mpx` gets the stand-in
 torch.cuda.set_device = lambda d: None
 torch.cuda.synchronize = lambda *a: None

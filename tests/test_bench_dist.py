@@ -45,6 +45,7 @@ def run(world, scenario, tmp_path):
 @pytest.mark.parametrize("world", [2, 4])
 def test_rounds_peers_and_expected_checksums(world, tmp_path):
     res = run(world, "ok", tmp_path)
+    assert all(d["spin"] for d in res)       # the shared-memory spin barrier carried every per-round barrier
     rounds = all_pairs_rounds(world)
     n, iters, steps, warmup = 4096, 7, 5, 2
     warmup = max(warmup, world - 1)          # pairs_bench warms every round up at least once

@@ -66,6 +66,7 @@ def test_one_json_line_with_the_contract_keys():
     assert d["config"]["ll_max"] == 8192 and d["extras"]["ll_choice"]["chosen_ll_max"] == 8192
     assert d["extras"]["unidir_4MiB_unstaged_GBps"] is not None
     assert d["extras"]["hbv3_rounds_unidir"]["phases_us_median"]["g1"]["kernel_s"] == 1.0
+    assert d["config"]["barrier"].startswith("node-local spin barrier") and d["config"]["launch"].startswith("armed")
 
 
 def test_hung_comparison_engine_cannot_cost_the_line():
