@@ -264,3 +264,17 @@ def test_link_counters_one_sampler_per_gpu(world, scenario, tmp_path):
                 inside = [x for x in log[i:j] if x[0] == "xfer"]
                 assert len(inside) == world - 1 and all((x[2], x[6], x[7], x[8]) == (2, iters, n, False)
                                                         for x in inside)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cpu_baseline_beside_the_pairs_line(world):
+    """The reference itself beside the N >= 2 line:
+    run-hbv3's layout (N ranks, -p N/2 -u 1) under MPICH shm at a small B,
+    aggregate = N/2 pairs' bytes / the slowest sender's time per run."""
+    ref = os.path.join(os.path.dirname(HERE), "oracle", "_ref", "mpi_perf")
+    if not os.path.exists(ref):
+        pytest.skip("compiled reference not built here (oracle/_ref)")
+    cb = bench.cpu_baseline_pairs(world, 1 << 20, 40, 3)
+    assert cb and cb["kind"] == "reference" and cb["cores"] == world and cb["unit"] == "GB/s"
+    assert cb["value"] > 0 and cb["per_pair_GBps"] == pytest.approx(cb["value"] / (world // 2), rel=1e-2)
+    assert f"{world} ranks, -p {world // 2} -u 1 -b {1 << 20} -i 40 -r 3" in cb["sample"]

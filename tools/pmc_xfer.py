@@ -84,3 +84,6 @@ if __name__ == "__main__":
     else:
         pair(sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[5]), int(sys.argv[6]), sys.argv[7] == "1",
              len(sys.argv) > 8 and sys.argv[8] == "pull")
+    # every context is finalized: the pooled rank streams go before exit (a
+    # profiler's exit-time finalizer faulted on them: r04_exit_segv_stack.txt)
+    mpx.shutdown()
