@@ -364,9 +364,12 @@ int mpxb_spin_open(mpxb_spin **out, const char *name, int nranks, int create)
     s->w = p;
     s->shared = 1;
     if (create) __atomic_store_n(&s->w->n, nranks, __ATOMIC_RELEASE);   /* (ftruncate zeroed the words) */
-    else if (__atomic_load_n(&s->w->n, __ATOMIC_ACQUIRE) != nranks) {
-        mpxb_spin_close(s, 0);
-        return err("spin barrier %s: made for %d ranks, not %d", name, s->w ? s->w->n : -1, nranks);
+    else {
+        const int made = __atomic_load_n(&s->w->n, __ATOMIC_ACQUIRE);
+        if (made != nranks) {
+            mpxb_spin_close(s, 0);
+            return err("spin barrier %s: made for %d ranks, not %d", name, made, nranks);
+        }
     }
     *out = s;
     return 0;
