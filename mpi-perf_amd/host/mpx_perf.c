@@ -744,7 +744,8 @@ int main(int argc, char **argv)
         rank_main((void *)(intptr_t)me);
         barrier(); /* MPI_Barrier, mpi_perf.c:579: no peer still maps our buffers */
         if (ctx) MPX_CHECK(mpx_finalize(ctx)); /* frees tx/rx too */
-        if (ctx) MPX_CHECK(mpx_shutdown()); /* pooled rank streams, before exit's teardown */
+        if (ctx && !getenv("MPX_PERF_NO_SHUTDOWN")) MPX_CHECK(mpx_shutdown()); /* pooled rank streams, before exit's teardown */
+        if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx_perf] rank %d: shut down\n", me);
         barrier();
         mpxb_spin_close(start_bar, 0);
         mpxb_finalize(boot);
