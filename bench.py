@@ -1417,11 +1417,16 @@ def main() -> None:
         if spin is not None:
             spin.close()
         dist.destroy_process_group()
-    # every context is finalized: the pooled rank streams go now, while the
-    # process is whole — left to the exit teardown, they made the counter
-    # tool's (rocprofiler-sdk's) exit-time finalizer fault in libhsa-runtime64
-    # (profiles/r04_exit_segv_stack.txt)
-    mpx.shutdown()
+    # Every context is finalized and the line is out: the process ends here,
+    # without the exit-time teardown of the HIP runtime and of the counter
+    # tool (the driver releases the process's GPU state).  That teardown
+    # faulted inside rocprofiler-sdk's finalizer while rank streams were
+    # alive (profiles/r04_exit_segv_stack.txt), and destroying them first
+    # (mpx_shutdown) stalled 1 processes-mode exit in 4 inside the runtime
+    # (profiles/r04_procs_exit_stall.txt).
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 if __name__ == "__main__":

@@ -744,8 +744,10 @@ int main(int argc, char **argv)
         rank_main((void *)(intptr_t)me);
         barrier(); /* MPI_Barrier, mpi_perf.c:579: no peer still maps our buffers */
         if (ctx) MPX_CHECK(mpx_finalize(ctx)); /* frees tx/rx too */
-        if (ctx && !getenv("MPX_PERF_NO_SHUTDOWN")) MPX_CHECK(mpx_shutdown()); /* pooled rank streams, before exit's teardown */
-        if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx_perf] rank %d: shut down\n", me);
+        /* the pooled rank streams are left to the runtime's exit teardown:
+           destroying them here (mpx_shutdown) stalled 1 exit in 4 in this
+           mode (profiles/r04_procs_exit_stall.txt), as round 3's exit-handler
+           destroy did */
         barrier();
         mpxb_spin_close(start_bar, 0);
         mpxb_finalize(boot);
@@ -767,10 +769,10 @@ int main(int argc, char **argv)
         }
     }
     if (ctx) MPX_CHECK(mpx_finalize(ctx));
-    /* the pooled rank streams go before exit: left to the HIP runtime's exit
-       teardown, a profiler tool's exit-time finalizer (rocprofiler-sdk, as
-       under rocprofv3 --pmc) faulted in libhsa-runtime64
-       (profiles/r04_exit_segv_stack.txt) */
+    /* one process, threads: the pooled rank streams go before exit — left
+       to the HIP runtime's exit teardown, a profiler tool's exit-time
+       finalizer (rocprofiler-sdk, as under rocprofv3 --pmc) faulted on them
+       in libhsa-runtime64 (profiles/r04_exit_segv_stack.txt) */
     if (ctx) MPX_CHECK(mpx_shutdown());
     return 0;
 }
