@@ -598,8 +598,10 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs, phases: 
         allp = [x for e in every for x in (e or [])]
         out["phases_us_median"] = {
             side: {k: round(statistics.median(p[k] for gg, p in allp if gg == g) * 1e6, 2) for k in allp[0][1]
-                   if k != "armed"}
+                   if k not in ("armed", "resident")}
             for side, g in (("g1", 1), ("g0", 0)) if any(gg == g for gg, _ in allp)} if allp else None
+        # armed calls whose whole grid was running when mpx_xfer_arm returned
+        out["resident_fraction"] = round(sum(p["resident"] for _, p in allp) / len(allp), 3) if allp else None
     return out
 
 

@@ -253,7 +253,9 @@ int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank
    region); hosts arm before their barrier (mpi_perf.c:499), so the kernel
    launch (~14 us on MI355X, profiles/r04_phases_query.jsonl) is no longer
    part of every short loop's recorded time.  The armed call's device_s is
-   the kernel's own clock from start to end.  A rank holds one armed call;
+   the kernel's own clock from start to end.  mpx_xfer_arm returns once the
+   kernel's whole grid runs and waits (at most 5 ms later), so the start does
+   not also pay the rest of the dispatch.  A rank holds one armed call;
    mpx_xfer_ex with other arguments fails (MPX_ERR_STATE) and leaves it
    armed.  The SDMA and RCCL engines accept the call and do nothing. */
 int mpx_xfer_arm(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
@@ -294,7 +296,9 @@ typedef struct mpx_phases {
     int32_t armed;            /* 1: the call was armed (mpx_xfer_arm): its
                                  launch happened before the call, and
                                  launch_to_start_s is go store -> running       */
-    int32_t reserved;
+    int32_t resident;         /* armed: 1 if every workgroup of the kernel was
+                                 running and waiting for the start when
+                                 mpx_xfer_arm returned (it waits up to 5 ms)   */
 } mpx_phases;
 int mpx_last_phases(mpx_ctx *ctx, int rank, mpx_phases *out);
 

@@ -80,6 +80,8 @@ struct Status {
     u64 go;                 // armed call (mpx_xfer_arm): the host stores the
                             // call's token here to start it, token | kGoCancel
                             // to end it without a transfer
+    u64 ready;              // armed call: its token once every workgroup is
+                            // resident and waiting for go
 };
 constexpr u64 kGoCancel = 1ull << 63;
 
@@ -92,8 +94,10 @@ constexpr u64 kGoCancel = 1ull << 63;
 //   [6..7] RCCL engine's one-byte link set-up exchange
 //   [8] armed call: workgroup 0's go verdict for the others (1 go, 2 cancel),
 //       reset with [0..3]
+//   [9] armed call: workgroups other than 0 waiting for go, reset with [0..3]
 constexpr int kScratchWords = 16;
-constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrLanded = 3, kScrSeqBase = 4, kScrLink = 6, kScrGo = 8;
+constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrLanded = 3, kScrSeqBase = 4, kScrLink = 6, kScrGo = 8,
+              kScrReady = 9;
 
 // Non-blocking check mode ("ring"): receive j of a call with `iters`
 // iterations lands in slot (iters-1-j) mod S of the receiver, where slot 0 is

@@ -462,6 +462,9 @@ struct Loop {
     // tx load on the latency path.
     u64 pre[kLLUnitsPerLane];
     u64* s_seen = nullptr;   // LDS, pull mode: the peer's ready word as last read
+    // a.stage: s_tx holds this workgroup's chunk once the first push (which
+    // reads tx from memory and fills s_tx on the way) is done
+    mutable bool staged = false;
 
     __device__ void preload_ll(long long n) {
 #pragma unroll
@@ -523,21 +526,15 @@ struct Loop {
         *hi = *lo + chunk < n ? *lo + chunk : n;
     }
 
-    // LDS staging (a.stage): each pushing workgroup copies its chunk's 16-B
-    // units of tx into LDS once per launch; every push then reads LDS
-    // (ds_read_b128) instead of HBM/L2, so the per-iteration critical path
-    // is LDS -> remote store.  tx is read-only while the loop runs.
-    __device__ void stage_tx(long long n) const {
-        if ((int)blockIdx.x >= a.nwg) return;
-        long long lo, hi;
-        chunk_of(n, &lo, &hi);
-        if (lo >= hi) return;
-        const int nv = (int)((hi - lo) >> 4);
-        const v4u* src = reinterpret_cast<const v4u*>(a.tx + lo);
-        for (int v = threadIdx.x; v < nv; v += kBlock) s_tx[v] = src[v];
-    }
-
-    template <int AUX>
+    // LDS staging (a.stage): each pushing workgroup keeps its chunk's 16-B
+    // units of tx in LDS for the whole launch; every push after the first
+    // reads LDS (ds_read_b128) instead of HBM/L2, so the per-iteration
+    // critical path is LDS -> remote store.  The first push reads tx from
+    // memory and fills LDS on the way (STAGE below): no separate staging pass
+    // stands between the start of the call and its first byte on the link.
+    // tx is read-only while the loop runs.  Lane t handles units t, t+kBlock,
+    // ... in every pass, so it reads back only LDS words it wrote itself.
+    template <int AUX, bool STAGE>
     __device__ __forceinline__ void push_units(const v4u* src, __amdgpu_buffer_rsrc_t dst, int nv) const {
         int v = threadIdx.x;
         for (; v + 3 * kBlock < nv; v += 4 * kBlock) {
@@ -546,8 +543,23 @@ struct Loop {
             __builtin_amdgcn_raw_buffer_store_b128(r1, dst, (v + kBlock) * 16, 0, AUX);
             __builtin_amdgcn_raw_buffer_store_b128(r2, dst, (v + 2 * kBlock) * 16, 0, AUX);
             __builtin_amdgcn_raw_buffer_store_b128(r3, dst, (v + 3 * kBlock) * 16, 0, AUX);
+            if (STAGE) {
+                s_tx[v] = r0;
+                s_tx[v + kBlock] = r1;
+                s_tx[v + 2 * kBlock] = r2;
+                s_tx[v + 3 * kBlock] = r3;
+            }
         }
-        for (; v < nv; v += kBlock) __builtin_amdgcn_raw_buffer_store_b128(src[v], dst, v * 16, 0, AUX);
+        for (; v < nv; v += kBlock) {
+            const v4u r = src[v];
+            __builtin_amdgcn_raw_buffer_store_b128(r, dst, v * 16, 0, AUX);
+            if (STAGE) s_tx[v] = r;
+        }
+    }
+    template <bool STAGE>
+    __device__ __forceinline__ void push_units_aux(const v4u* src, __amdgpu_buffer_rsrc_t dst, int nv) const {
+        if (a.stream) push_units<kAuxSysNt, STAGE>(src, dst, nv);
+        else push_units<kAuxSys, STAGE>(src, dst, nv);
     }
 
     // publish = false: the stores are issued but not drained and no flag is
@@ -560,19 +572,27 @@ struct Loop {
         if (w >= a.nwg) return;
         long long lo, hi;
         chunk_of(n, &lo, &hi);
-        if (lo < hi && !skip) {
+        if (lo < hi) {
             const unsigned bytes = (unsigned)(hi - lo);
             const __amdgpu_buffer_rsrc_t dst = rsrc((dst_base ? dst_base : a.peer_rx) + lo, bytes);
             const int nv = (int)(bytes >> 4);
-            const v4u* src = a.stage ? s_tx : reinterpret_cast<const v4u*>(a.tx + lo);
-            if (a.stream) push_units<kAuxSysNt>(src, dst, nv);
-            else push_units<kAuxSys>(src, dst, nv);
+            const v4u* txv = reinterpret_cast<const v4u*>(a.tx + lo);
+            if (a.stage && !staged) {
+                if (!skip) {
+                    push_units_aux<true>(txv, dst, nv);
+                } else {
+                    for (int v = threadIdx.x; v < nv; v += kBlock) s_tx[v] = txv[v];   // stage only
+                }
+            } else if (!skip) {
+                push_units_aux<false>(a.stage ? s_tx : txv, dst, nv);
+            }
             const unsigned tail = bytes & 15;
-            if (threadIdx.x < tail) {
+            if (threadIdx.x < tail && !skip) {
                 const unsigned o = (unsigned)nv * 16 + threadIdx.x;
                 __builtin_amdgcn_raw_buffer_store_b8(a.tx[lo + o], dst, o, 0, kAuxSys);
             }
         }
+        staged = true;
         if (!publish) return;
         drain_stores();                 // every storing wave
         __syncthreads();
@@ -813,6 +833,11 @@ struct Loop {
     // Workgroup 0 polls the host word and hands its verdict to the others in
     // scratch word kScrGo.  False: cancelled (mpx_xfer_disarm) or no start
     // within go_timeout_ticks (then Status.err = 2): no transfer at all.
+    // Every other workgroup counts itself in (kScrReady) when it starts to
+    // wait; once all have, workgroup 0 stores the token into Status.ready —
+    // the whole grid is resident and waiting — which mpx_xfer_arm waits for,
+    // so a start right after the host's barrier does not also pay the rest of
+    // the launch.
     __device__ bool wait_go() const {
         if (!a.go_token) return true;
         __shared__ int s_go;
@@ -820,7 +845,13 @@ struct Loop {
             const u64 t0 = now_ticks();
             u64 spins = 0, w = 0;
             if (blockIdx.x == 0) {
+                bool told = false;
                 for (;;) {
+                    if (!told && __hip_atomic_load(&a.gbar[kScrReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                     (u64)gridDim.x - 1) {
+                        st_sys(&a.status->ready, a.go_token);
+                        told = true;
+                    }
                     const u64 v = ld_sys(&a.status->go);
                     if (v == a.go_token) { w = 1; break; }
                     if (v == (a.go_token | kGoCancel)) { w = 2; break; }
@@ -833,6 +864,7 @@ struct Loop {
                 }
                 __hip_atomic_store(&a.gbar[kScrGo], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
+                __hip_atomic_fetch_add(&a.gbar[kScrReady], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // (workgroup 0 answers within its own deadline; one second
                 // more bounds this wait should it never run)
                 while ((w = __hip_atomic_load(&a.gbar[kScrGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
@@ -874,6 +906,7 @@ struct Loop {
         if (threadIdx.x != 0) return;
         for (int k = 0; k < 4; ++k) __hip_atomic_store(&a.gbar[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.gbar[kScrGo], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.gbar[kScrReady], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         st_sys(&a.status->t_exit, now_ticks());
         drain_stores();
         st_sys(&a.status->done, a.done_token);
@@ -1149,8 +1182,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     }
     L.stamp(&a.status->t_entry);
     const long long n = a.len;
-    if (a.stage) L.stage_tx(n);
-    __syncthreads();
     // the size this side sends: B, or the 1-byte ack of unidir group 0
     const long long send_len = (MODE == MPX_MODE_UNIDIR && GROUP == 0) ? 1 : n;
     const bool ll_send = blockIdx.x == 0 && L.is_ll(send_len);
@@ -1249,8 +1280,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     }
     L.stamp(&a.status->t_entry);
     const long long n = a.len;
-    if (a.stage) L.stage_tx(n);
-    __syncthreads();
     const int w = blockIdx.x;
     const u64 fmix = mix64((u64)n);
     const u64* credit = &a.my_mb->credit[a.peer_slot][w];

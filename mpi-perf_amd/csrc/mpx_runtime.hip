@@ -595,6 +595,7 @@ struct KernelCall {
     uint32_t timeout_ms = 0;
     uint64_t expect = 0, expect_ack = 0;
     double t_launch = 0;
+    bool resident = false;   // armed: every workgroup was waiting when arm returned
 };
 
 // Wait for the call's completion.  Unarmed: the end event ev1 (see
@@ -759,6 +760,7 @@ int launch_call(Rank& me, KernelCall& kc, bool armed) {
     me.status->recv_digest = 0;
     me.status->t_entry = me.status->t_posted = me.status->t_exit = 0;
     if (armed) {
+        __atomic_store_n(&me.status->ready, 0ull, __ATOMIC_RELAXED);
         a.go_token = a.done_token;
         // the host's barrier sits between arm and start: bounded generously
         a.go_timeout_ticks = std::max<u64>(a.timeout_ticks, 60ull * 100000000ull);
@@ -810,6 +812,7 @@ int complete_call(Rank& me, KernelCall& kc, bool armed, double t_call, double t0
         ph.done_to_return_s = t_end - t_done;
     }
     ph.armed = armed ? 1 : 0;
+    ph.resident = (armed && kc.resident) ? 1 : 0;
     const unsigned err = __atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE);
     if (err == 2) {
         me.broken = true;
@@ -1871,6 +1874,8 @@ bool armed_matches(const KernelCall& kc, int mode, int group, int peer_rank, int
 }
 }  // namespace
 
+constexpr double kArmReadyWaitS = 5e-3;
+
 int mpx_xfer_arm(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_rank, int iters, void* tx, void* rx,
                  int buff_len, const mpx_xfer_opts* opts) {
     if (!ctx) return fail(MPX_ERR_INVALID, "NULL argument");
@@ -1888,6 +1893,14 @@ int mpx_xfer_arm(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_ran
         delete kc;
         return st;
     }
+    // Until the whole grid runs (Status.ready), a start would also wait for
+    // the rest of the launch (the dispatch of every workgroup, ~5-10 us after
+    // the launch call): wait for it here, ahead of the host's barrier.  The
+    // wait is bounded (a grid that cannot all be resident yet, e.g. ranks
+    // sharing a busy GPU, still starts correctly, only later).
+    const double until = now_s() + kArmReadyWaitS;
+    while (!(kc->resident = __atomic_load_n(&me.status->ready, __ATOMIC_ACQUIRE) == kc->a.go_token) && now_s() < until)
+        cpu_relax();
     me.armed = kc;
     return MPX_OK;
 }

@@ -72,10 +72,10 @@ class XferOpts(C.Structure):
 
 class Phases(C.Structure):
     _fields_ = [(k, C.c_double) for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",
-                                           "done_to_return_s")] + [("armed", C.c_int32), ("reserved", C.c_int32)]
+                                           "done_to_return_s")] + [("armed", C.c_int32), ("resident", C.c_int32)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 def pattern_key(seed: int, src: int, dst: int, it: int) -> int:

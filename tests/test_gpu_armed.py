@@ -36,6 +36,8 @@ def test_armed_calls_match_unarmed(mode, pull):
                 for r in (0, 1):
                     assert out[r].check_failures == 0 and out[r].check_iters == iters
                     assert P.c.phases(r)["armed"] == (1 if armed else 0)
+                    if not armed:
+                        assert P.c.phases(r)["resident"] == 0
                 res.setdefault("sig", (out[0].recv_done, out[0].recv_digest, out[1].recv_done, out[1].recv_digest))
                 assert (out[0].recv_done, out[0].recv_digest, out[1].recv_done, out[1].recv_digest) == res["sig"]
                 for r in (0, 1):
@@ -56,6 +58,8 @@ def test_armed_phases_exclude_the_launch():
         for r in (0, 1):
             ph = P.c.phases(r)
             assert ph["armed"] == 1 and ph["host_prep_s"] == 0
+            # two small grids on one GPU: both fully running before the start
+            assert ph["resident"] == 1
             assert 0 < ph["kernel_s"] <= ph["wall_s"]
             assert out[r].device_s == pytest.approx(ph["kernel_s"])
     finally:

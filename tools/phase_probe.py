@@ -64,7 +64,8 @@ with mpx.Context(2, "kernel") as c:
             rec["pair_wall_us_median"] = round(statistics.median(walls) * 1e6, 2)
             for r, label in ((0, "g1"), (1, "g0")):
                 rec[label] = {k: round(statistics.median(x[k] for x in rows[r]) * 1e6, 2) for k in rows[r][0]
-                              if k != "armed"}
+                              if k not in ("armed", "resident")}
+                rec[label]["resident_fraction"] = sum(x["resident"] for x in rows[r]) / len(rows[r])
             if mode == mpx.MODE_UNIDIR:
                 rec["GBps"] = round(n * iters / statistics.median(walls) / 1e9, 2)
         print(json.dumps(rec), flush=True)
