@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MPX_ABI_VERSION 6
+#define MPX_ABI_VERSION 7
 #define MPX_MAX_RANKS 64          /* ranks one context can address           */
 #define MPX_RANK_DESC_BYTES 512   /* size of the opaque exported descriptor  */
 #define MPX_RCCL_ID_BYTES 128     /* size of an RCCL unique id               */
@@ -299,6 +299,12 @@ typedef struct mpx_phases {
     int32_t resident;         /* armed: 1 if every workgroup of the kernel was
                                  running and waiting for the start when
                                  mpx_xfer_arm returned (it waits up to 5 ms)   */
+    double first_iter_s;      /* the loop's first iteration, from the kernel's
+                                 start (or the peer's post, sides that push
+                                 first) to its end (workgroup 0; ping-pong and
+                                 unidir loops, else 0)                          */
+    double tail_s;            /* workgroup 0 left the loop -> the last
+                                 workgroup's end (accounting, resets)           */
 } mpx_phases;
 int mpx_last_phases(mpx_ctx *ctx, int rank, mpx_phases *out);
 

@@ -82,6 +82,8 @@ struct Status {
                             // to end it without a transfer
     u64 ready;              // armed call: its token once every workgroup is
                             // resident and waiting for go
+    u64 t_first;            // workgroup 0 finished the loop's first iteration
+    u64 t_loop;             // workgroup 0 left the loop
 };
 constexpr u64 kGoCancel = 1ull << 63;
 

@@ -1209,6 +1209,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (a.check) L.check(n, i);
                 L.send(n, ++txs, skip);                // Send(tx, B, tag 2)
             }
+            if (i == 0) L.stamp(&a.status->t_first);
         } else if constexpr (MODE == MPX_MODE_UNIDIR) {  // mpi_perf.c:132-144
             if constexpr (GROUP == 1) {
                 L.send(n, ++txs, skip);                // Send(tx, B)
@@ -1221,6 +1222,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (a.check) { L.check(n, i); if (!L.grid_sync(i)) break; }
                 L.send(1, ++txs, skip);                // Send(tx, 1)
             }
+            if (i == 0) L.stamp(&a.status->t_first);
         } else {                                       // mpi_perf.c:95-124
             // Isend + Irecv, slot `inflight`.  A receiver waits only at the
             // window flush (i = 255 mod 256) and at the end, so a push needs
@@ -1244,6 +1246,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
             }
         }
     }
+    L.stamp(&a.status->t_loop);
     if constexpr (MODE == MPX_MODE_NONBLOCKING) {
         if (inflight > 0 && !L.aborted() && L.wait_bulk(rxs + a.iters, a.iters - 1))   // final Waitall(inflight)
             done += (u64)inflight;

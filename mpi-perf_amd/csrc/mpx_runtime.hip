@@ -759,6 +759,7 @@ int launch_call(Rank& me, KernelCall& kc, bool armed) {
     me.status->recv_done = 0;
     me.status->recv_digest = 0;
     me.status->t_entry = me.status->t_posted = me.status->t_exit = 0;
+    me.status->t_first = me.status->t_loop = 0;
     if (armed) {
         __atomic_store_n(&me.status->ready, 0ull, __ATOMIC_RELAXED);
         a.go_token = a.done_token;
@@ -813,6 +814,13 @@ int complete_call(Rank& me, KernelCall& kc, bool armed, double t_call, double t0
     }
     ph.armed = armed ? 1 : 0;
     ph.resident = (armed && kc.resident) ? 1 : 0;
+    // inside the kernel (k_xfer): the first iteration from the moment this
+    // side could start it, and the end after the loop
+    const u64 tf = __atomic_load_n(&me.status->t_first, __ATOMIC_ACQUIRE);
+    const u64 tl = __atomic_load_n(&me.status->t_loop, __ATOMIC_ACQUIRE);
+    const u64 t_go = tp >= te ? tp : te;
+    ph.first_iter_s = (te && tf >= t_go) ? (double)(tf - t_go) * 1e-8 : 0;
+    ph.tail_s = (tl && tx >= tl) ? (double)(tx - tl) * 1e-8 : 0;
     const unsigned err = __atomic_load_n(&me.status->err, __ATOMIC_ACQUIRE);
     if (err == 2) {
         me.broken = true;

@@ -31,7 +31,7 @@ FILL_BYTE, FILL_SPLITMIX = 0, 1
 XFER_STREAM = 1
 XFER_PULL = 2
 XFER_NOSTAGE = 4
-ABI_VERSION = 6
+ABI_VERSION = 7
 PATTERN_SEED = 0x6D70695F70657266
 MAX_RANKS = 64
 RANK_DESC_BYTES = 512
@@ -71,8 +71,9 @@ class XferOpts(C.Structure):
 
 
 class Phases(C.Structure):
-    _fields_ = [(k, C.c_double) for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",
-                                           "done_to_return_s")] + [("armed", C.c_int32), ("resident", C.c_int32)]
+    _fields_ = ([(k, C.c_double) for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",
+                                            "done_to_return_s")]
+                + [("armed", C.c_int32), ("resident", C.c_int32), ("first_iter_s", C.c_double), ("tail_s", C.c_double)])
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -129,7 +129,7 @@ class FakeMpx:
 
         def phases(self, r):
             return dict({k: 1e-6 for k in ("wall_s", "host_prep_s", "launch_to_start_s", "posted_wait_s", "kernel_s",
-                                           "done_to_return_s")}, armed=1, resident=1)
+                                           "done_to_return_s", "first_iter_s", "tail_s")}, armed=1, resident=1)
 
         def prepare(self, mode, group, me, peer, iters, n, timeout_ms=0, pull=False):
             FakeMpx.log.append(["prepare", self.engine, mode, group, me, peer, iters, n, pull])

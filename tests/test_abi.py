@@ -45,7 +45,7 @@ def test_version_and_strerror():
     # 2: recv_done / recv_digest; 3: 64 ranks per context; 4: receive-posted mailbox word;
     # 5: pull mode (MPX_XFER_PULL, tx in the rank descriptor); 6: mpx_last_phases,
     # mpx_device_bus_id, MPX_XFER_NOSTAGE, kernel-cleared scratch words
-    assert L.mpx_version() == 6
+    assert L.mpx_version() == 7
     texts = {L.mpx_strerror(i).decode() for i in range(9)}
     assert len(texts) == 9
     assert L.mpx_strerror(12345) == b"unknown mpx status"

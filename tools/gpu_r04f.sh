@@ -5,7 +5,7 @@
 # the N=2 one-GPU rehearsal (hbv3_rounds_unidir vs round0_sweep).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04f
+O=gpurun_out/${R04_OUT:-r04f}
 mkdir -p $O
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_armed.py tests/test_gpu_engine.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
