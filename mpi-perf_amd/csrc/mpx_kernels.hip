@@ -720,7 +720,7 @@ struct Loop {
                 __builtin_amdgcn_s_sleep(1);
             }
         }
-        stamp(&a.status->t_posted);
+        stamp(kScrTPosted);
         __syncthreads();
         return !aborted();
     }
@@ -883,8 +883,11 @@ struct Loop {
     // and, on a side that pushes first, the moment the peer's receives were
     // seen posted (t_posted): the host splits a call's wall time into launch,
     // wait for the peer, transfer and completion with them (mpx_last_phases).
-    __device__ void stamp(u64* field) const {
-        if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(field, now_ticks());
+    // The stamps go to device scratch words (kScrTEntry..kScrTLoop); the last
+    // workgroup copies them into the host-mapped status at the end.
+    __device__ void stamp(int word) const {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(&a.gbar[word], now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // Every workgroup calls it last; true (uniformly) in the one that
     // finishes last — every other workgroup is done with the scratch words
@@ -904,10 +907,16 @@ struct Loop {
     // word the host spins on (Status.done = this call's token).
     __device__ void finish_last() const {
         if (threadIdx.x != 0) return;
+        const u64 t_end = now_ticks();
         for (int k = 0; k < 4; ++k) __hip_atomic_store(&a.gbar[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.gbar[kScrGo], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.gbar[kScrReady], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        st_sys(&a.status->t_exit, now_ticks());
+        u64* const ts[4] = {&a.status->t_entry, &a.status->t_posted, &a.status->t_first, &a.status->t_loop};
+        for (int k = 0; k < 4; ++k) {
+            st_sys(ts[k], __hip_atomic_load(&a.gbar[kScrTEntry + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            __hip_atomic_store(&a.gbar[kScrTEntry + k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        st_sys(&a.status->t_exit, t_end);
         drain_stores();
         st_sys(&a.status->done, a.done_token);
     }
@@ -1180,7 +1189,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
         if (L.last_to_finish()) L.finish_last();
         return;
     }
-    L.stamp(&a.status->t_entry);
+    L.stamp(kScrTEntry);
     const long long n = a.len;
     // the size this side sends: B, or the 1-byte ack of unidir group 0
     const long long send_len = (MODE == MPX_MODE_UNIDIR && GROUP == 0) ? 1 : n;
@@ -1209,7 +1218,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (a.check) L.check(n, i);
                 L.send(n, ++txs, skip);                // Send(tx, B, tag 2)
             }
-            if (i == 0) L.stamp(&a.status->t_first);
+            if (i == 0) L.stamp(kScrTFirst);
         } else if constexpr (MODE == MPX_MODE_UNIDIR) {  // mpi_perf.c:132-144
             if constexpr (GROUP == 1) {
                 L.send(n, ++txs, skip);                // Send(tx, B)
@@ -1222,7 +1231,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (a.check) { L.check(n, i); if (!L.grid_sync(i)) break; }
                 L.send(1, ++txs, skip);                // Send(tx, 1)
             }
-            if (i == 0) L.stamp(&a.status->t_first);
+            if (i == 0) L.stamp(kScrTFirst);
         } else {                                       // mpi_perf.c:95-124
             // Isend + Irecv, slot `inflight`.  A receiver waits only at the
             // window flush (i = 255 mod 256) and at the end, so a push needs
@@ -1246,7 +1255,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
             }
         }
     }
-    L.stamp(&a.status->t_loop);
+    L.stamp(kScrTLoop);
     if constexpr (MODE == MPX_MODE_NONBLOCKING) {
         if (inflight > 0 && !L.aborted() && L.wait_bulk(rxs + a.iters, a.iters - 1))   // final Waitall(inflight)
             done += (u64)inflight;
@@ -1281,7 +1290,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
         if (L.last_to_finish()) L.finish_last();
         return;
     }
-    L.stamp(&a.status->t_entry);
+    L.stamp(kScrTEntry);
     const long long n = a.len;
     const int w = blockIdx.x;
     const u64 fmix = mix64((u64)n);
@@ -1296,7 +1305,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     // call's last credits already satisfy this call's first S pushes.
     L.post_receives();
     bool ok = a.iters == 0 || L.nb_wait([&] { return threadIdx.x != 0 || L.peer_posted(); }, &next, 0);
-    L.stamp(&a.status->t_posted);
+    L.stamp(kScrTPosted);
     for (int i = 0; i < a.iters && ok; ++i) {
         // slot ring_slot(i) was last used by push i - S of this call: wait
         // for its credit
@@ -1354,7 +1363,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
         if (L.last_to_finish()) L.finish_last();
         return;
     }
-    L.stamp(&a.status->t_entry);
+    L.stamp(kScrTEntry);
     const long long n = a.len;
     const u64 nw = (u64)a.nwg;
     if (MODE == MPX_MODE_UNIDIR && GROUP == 0 && blockIdx.x == 0) L.preload_ll(1);   // the ack's byte
