@@ -84,8 +84,8 @@ struct Status {
                             // resident and waiting for go
     u64 t_first;            // workgroup 0 finished the loop's first iteration
     u64 t_loop;             // workgroup 0 left the loop
-                            // (t_entry, t_posted, t_first, t_loop: copied from
-                            // device scratch [10..13] at the end of the call)
+                            // (t_entry, t_posted, t_first, t_loop: workgroup 0
+                            // stores them at the end of the call)
 };
 constexpr u64 kGoCancel = 1ull << 63;
 
@@ -99,13 +99,9 @@ constexpr u64 kGoCancel = 1ull << 63;
 //   [8] armed call: workgroup 0's go verdict for the others (1 go, 2 cancel),
 //       reset with [0..3]
 //   [9] armed call: workgroups other than 0 waiting for go, reset with [0..3]
-//   [10..13] kernel-engine call phases (s_memrealtime): entry, posted, first
-//       iteration done, loop left — stamped by workgroup 0 into device memory
-//       (a store to host memory would make the next drain wait for its PCIe
-//       round trip), copied into Status by the last workgroup and reset
 constexpr int kScratchWords = 16;
 constexpr int kScrBar = 0, kScrAbort = 1, kScrFin = 2, kScrLanded = 3, kScrSeqBase = 4, kScrLink = 6, kScrGo = 8,
-              kScrReady = 9, kScrTEntry = 10, kScrTPosted = 11, kScrTFirst = 12, kScrTLoop = 13;
+              kScrReady = 9;
 
 // Non-blocking check mode ("ring"): receive j of a call with `iters`
 // iterations lands in slot (iters-1-j) mod S of the receiver, where slot 0 is

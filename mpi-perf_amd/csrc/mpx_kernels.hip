@@ -449,6 +449,9 @@ __global__ void k_seqbase(u64* base, u64 tx, u64 rx, int add) {
 // k_xfer: the transfer loop.  One launch runs all `iters` iterations of one
 // rank's side; the peer runs its own launch on its own GPU at the same time.
 // ---------------------------------------------------------------------------
+// phase stamps of workgroup 0 (Loop::ts)
+enum { kTsEntry = 0, kTsPosted = 1, kTsFirst = 2, kTsLoop = 3 };
+
 template <int MODE>
 struct Loop {
     const XferArgs& a;
@@ -465,6 +468,7 @@ struct Loop {
     // a.stage: s_tx holds this workgroup's chunk once the first push (which
     // reads tx from memory and fills s_tx on the way) is done
     mutable bool staged = false;
+    mutable u64 ts[4] = {0, 0, 0, 0};   // workgroup 0's phase stamps (stamp)
 
     __device__ void preload_ll(long long n) {
 #pragma unroll
@@ -720,7 +724,7 @@ struct Loop {
                 __builtin_amdgcn_s_sleep(1);
             }
         }
-        stamp(kScrTPosted);
+        stamp(kTsPosted);
         __syncthreads();
         return !aborted();
     }
@@ -883,40 +887,46 @@ struct Loop {
     // and, on a side that pushes first, the moment the peer's receives were
     // seen posted (t_posted): the host splits a call's wall time into launch,
     // wait for the peer, transfer and completion with them (mpx_last_phases).
-    // The stamps go to device scratch words (kScrTEntry..kScrTLoop); the last
-    // workgroup copies them into the host-mapped status at the end.
-    __device__ void stamp(int word) const {
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            __hip_atomic_store(&a.gbar[word], now_ticks(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // The stamps stay in workgroup 0's registers (ts) until it ends the call
+    // (finish_last): a store to host memory here would make the loop's next
+    // drain wait for its PCIe round trip.
+    __device__ void stamp(int k) const {
+        if (blockIdx.x == 0 && threadIdx.x == 0) ts[k] = now_ticks();
     }
-    // Every workgroup calls it last; true (uniformly) in the one that
-    // finishes last — every other workgroup is done with the scratch words
-    // and the status fields by then.
+    // Every workgroup calls it last.  Workgroup 0 ends the call: the others
+    // count themselves out (release) and exit; workgroup 0 waits until all
+    // have (acquire) — they are done with the scratch words, the status
+    // fields and their checksums by then — and returns true.  The others end
+    // early where they can (the last receive of a side that only waits for
+    // it, see k_xfer), so their count is usually in before workgroup 0 looks.
     __device__ bool last_to_finish() const {
-        __shared__ int s_last;
         __syncthreads();
         if (gridDim.x == 1) return true;   // (no counter round trip for a 1-workgroup grid)
+        if (blockIdx.x != 0) {
+            if (threadIdx.x == 0)
+                __hip_atomic_fetch_add(&a.gbar[kScrFin], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
         if (threadIdx.x == 0)
-            s_last = __hip_atomic_fetch_add(&a.gbar[kScrFin], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-                     (u64)gridDim.x - 1;
+            while (__hip_atomic_load(&a.gbar[kScrFin], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != (u64)gridDim.x - 1)
+                __builtin_amdgcn_s_sleep(1);
         __syncthreads();
-        return s_last != 0;
+        return true;
     }
-    // The last workgroup: scratch words [0..3] back to zero for the rank's
-    // next call (so no memset precedes a launch), the call's exit time, then
-    // — after every status store of the call has drained — the completion
-    // word the host spins on (Status.done = this call's token).
+    // Workgroup 0, last: scratch words [0..3] back to zero for the rank's
+    // next call (so no memset precedes a launch), the call's phase stamps and
+    // exit time, then — after every status store of the call has drained —
+    // the completion word the host spins on (Status.done = this call's token).
     __device__ void finish_last() const {
         if (threadIdx.x != 0) return;
         const u64 t_end = now_ticks();
         for (int k = 0; k < 4; ++k) __hip_atomic_store(&a.gbar[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.gbar[kScrGo], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.gbar[kScrReady], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        u64* const ts[4] = {&a.status->t_entry, &a.status->t_posted, &a.status->t_first, &a.status->t_loop};
-        for (int k = 0; k < 4; ++k) {
-            st_sys(ts[k], __hip_atomic_load(&a.gbar[kScrTEntry + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            __hip_atomic_store(&a.gbar[kScrTEntry + k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        st_sys(&a.status->t_entry, ts[kTsEntry]);
+        st_sys(&a.status->t_posted, ts[kTsPosted]);
+        st_sys(&a.status->t_first, ts[kTsFirst]);
+        st_sys(&a.status->t_loop, ts[kTsLoop]);
         st_sys(&a.status->t_exit, t_end);
         drain_stores();
         st_sys(&a.status->done, a.done_token);
@@ -1190,7 +1200,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
         if (L.last_to_finish()) L.finish_last();
         return;
     }
-    L.stamp(kScrTEntry);
+    L.stamp(kTsEntry);
     const long long n = a.len;
     // the size this side sends: B, or the 1-byte ack of unidir group 0
     const long long send_len = (MODE == MPX_MODE_UNIDIR && GROUP == 0) ? 1 : n;
@@ -1205,11 +1215,17 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     // peer sent after it saw this side's post, so its peer has started too.
     constexpr bool push_first = MODE == MPX_MODE_NONBLOCKING || GROUP == 1;
     const bool go = !push_first || a.iters == 0 || L.wait_posted();
+    // Group 1's last receive (ping-pong, unidir) without check mode: only
+    // workgroup 0 waits for it (it counts receives and ends the call); the
+    // others have nothing left to do once their last push is out, so they
+    // leave, and their finish count is in before workgroup 0 needs it.
+    const bool last_recv_wg0 = !a.check && blockIdx.x != 0;
     for (int i = 0; go && i < a.iters; ++i) {
         const bool skip = a.skip_push == i + 1;        // test knob only
         if constexpr (MODE == MPX_MODE_PINGPONG) {    // mpi_perf.c:70-82
             if constexpr (GROUP == 1) {
                 L.send(n, ++txs, skip);                // Send(tx, B, tag 1)
+                if (i + 1 == a.iters && last_recv_wg0) break;
                 if (!L.recv(n, ++rxs, i)) break;       // Recv(rx, B, tag 2)
                 ++done;
                 if (a.check) L.check(n, i);
@@ -1219,10 +1235,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (a.check) L.check(n, i);
                 L.send(n, ++txs, skip);                // Send(tx, B, tag 2)
             }
-            if (i == 0) L.stamp(kScrTFirst);
+            if (i == 0) L.stamp(kTsFirst);
         } else if constexpr (MODE == MPX_MODE_UNIDIR) {  // mpi_perf.c:132-144
             if constexpr (GROUP == 1) {
                 L.send(n, ++txs, skip);                // Send(tx, B)
+                if (i + 1 == a.iters && last_recv_wg0) break;
                 if (!L.recv(1, ++rxs, i)) break;       // Recv(rx, 1) — the ack
                 ++done;
                 if (a.check) L.check(1, i);
@@ -1232,7 +1249,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
                 if (a.check) { L.check(n, i); if (!L.grid_sync(i)) break; }
                 L.send(1, ++txs, skip);                // Send(tx, 1)
             }
-            if (i == 0) L.stamp(kScrTFirst);
+            if (i == 0) L.stamp(kTsFirst);
         } else {                                       // mpi_perf.c:95-124
             // Isend + Irecv, slot `inflight`.  A receiver waits only at the
             // window flush (i = 255 mod 256) and at the end, so a push needs
@@ -1256,7 +1273,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
             }
         }
     }
-    L.stamp(kScrTLoop);
+    L.stamp(kTsLoop);
     if constexpr (MODE == MPX_MODE_NONBLOCKING) {
         if (inflight > 0 && !L.aborted() && L.wait_bulk(rxs + a.iters, a.iters - 1))   // final Waitall(inflight)
             done += (u64)inflight;
@@ -1291,7 +1308,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
         if (L.last_to_finish()) L.finish_last();
         return;
     }
-    L.stamp(kScrTEntry);
+    L.stamp(kTsEntry);
     const long long n = a.len;
     const int w = blockIdx.x;
     const u64 fmix = mix64((u64)n);
@@ -1306,7 +1323,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     // call's last credits already satisfy this call's first S pushes.
     L.post_receives();
     bool ok = a.iters == 0 || L.nb_wait([&] { return threadIdx.x != 0 || L.peer_posted(); }, &next, 0);
-    L.stamp(kScrTPosted);
+    L.stamp(kTsPosted);
     for (int i = 0; i < a.iters && ok; ++i) {
         // slot ring_slot(i) was last used by push i - S of this call: wait
         // for its credit
@@ -1364,7 +1381,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
         if (L.last_to_finish()) L.finish_last();
         return;
     }
-    L.stamp(kScrTEntry);
+    L.stamp(kTsEntry);
     const long long n = a.len;
     const u64 nw = (u64)a.nwg;
     if (MODE == MPX_MODE_UNIDIR && GROUP == 0 && blockIdx.x == 0) L.preload_ll(1);   // the ack's byte
