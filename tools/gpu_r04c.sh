@@ -4,7 +4,7 @@
 # N=1 bench with in-process counters and the N=2 one-GPU rehearsal.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04c
+O=gpurun_out/${R04_OUT:-r04c}
 mkdir -p $O
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_armed.py -x -v --timeout 120 --timeout-method thread > $O/pytest_armed.log 2>&1
 rc=$?; echo "armed tests rc=$rc"; tail -3 $O/pytest_armed.log; [ $rc -eq 0 ] || exit $rc
