@@ -57,8 +57,45 @@ struct Mailbox {
     u64 ready[MPX_MAX_RANKS];
 };
 
+// The end of a kernel-engine call: ONE 64-byte line of the host-mapped
+// status, written by workgroup 0 with a single eight-lane store once every
+// other store of the call has drained (Loop::finish_last).  The host spins on
+// `word` = (u32)token | seal << 32, where the seal hashes the other seven
+// words with the token: a line that became visible piecemeal does not match
+// and is read again.  No drain sits between the line's fields and the word
+// the host waits for — one PCIe write instead of a write, an
+// acknowledgement and another write at the end of every call.
+struct alignas(64) Fin {
+    u64 recv_done;          // receives completed
+    u64 recv_digest;        // check mode: sum of their finished checksums
+    // phases (s_memrealtime, 100 MHz ticks), stamped by workgroup 0:
+    u64 t_entry;            // started (after the go of an armed call)
+    u64 t_posted;           // this side may push: the peer's receives are
+                            // posted (0: this side pushes only after a receive)
+    u64 t_first;            // the loop's first iteration done
+    u64 t_loop;             // left the loop
+    u64 t_exit;             // the call's end (every workgroup done)
+    u64 word;               // fin_word(...): the host's completion word
+};
+__host__ __device__ inline u64 fin_mix(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline u64 fin_word(u64 token, u64 v0, u64 v1, u64 v2, u64 v3, u64 v4, u64 v5, u64 v6) {
+    u64 h = fin_mix(token ^ 0x6a09e667f3bcc909ull);
+    h = fin_mix(h ^ v0);
+    h = fin_mix(h ^ v1);
+    h = fin_mix(h ^ v2);
+    h = fin_mix(h ^ v3);
+    h = fin_mix(h ^ v4);
+    h = fin_mix(h ^ v5);
+    h = fin_mix(h ^ v6);
+    return (token & 0xffffffffull) | (h << 32);
+}
+
 // Per-rank host-mapped status words (written by the device, read by the host
-// after the stream drains).
+// after the stream drains, or — the kernel engine — once `fin` is sealed).
 struct Status {
     unsigned int err;       // bit0: a wait timed out
     unsigned int where;     // 1 + iteration index of the first timeout
@@ -66,26 +103,16 @@ struct Status {
     // receive accounting of the last call, counted on the device where the
     // reference's call returns a receive (Recv, or Waitall for the
     // non-blocking loop, mpi_perf.c:75,79,110-111,122-123,137,141)
-    u64 recv_done;          // receives completed
-    u64 recv_digest;        // check mode: sum of their finished checksums
+    u64 recv_done;          // receives completed (stream engines; the kernel
+    u64 recv_digest;        // engine's are in fin) / check mode digest
     u64 seen, want;         // stream engines: flag value seen / awaited by the
                             // wait that timed out (diagnostics)
-    // kernel engine, phases of the last call (s_memrealtime, 100 MHz ticks):
-    u64 t_entry;            // workgroup 0 started
-    u64 t_posted;           // this side may push: the peer's receives are
-                            // posted (0: this side pushes only after a receive)
-    u64 t_exit;             // the last workgroup finished
-    u64 done;               // XferArgs.done_token, stored by the last workgroup
-                            // after everything else (the host's completion word)
     u64 go;                 // armed call (mpx_xfer_arm): the host stores the
                             // call's token here to start it, token | kGoCancel
                             // to end it without a transfer
     u64 ready;              // armed call: its token once every workgroup is
                             // resident and waiting for go
-    u64 t_first;            // workgroup 0 finished the loop's first iteration
-    u64 t_loop;             // workgroup 0 left the loop
-                            // (t_entry, t_posted, t_first, t_loop: workgroup 0
-                            // stores them at the end of the call)
+    Fin fin;                // kernel engine: the end of the last call
 };
 constexpr u64 kGoCancel = 1ull << 63;
 

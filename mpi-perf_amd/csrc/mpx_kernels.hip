@@ -469,6 +469,8 @@ struct Loop {
     // reads tx from memory and fills s_tx on the way) is done
     mutable bool staged = false;
     mutable u64 ts[4] = {0, 0, 0, 0};   // workgroup 0's phase stamps (stamp)
+    mutable u64 rdone = 0, rdig = 0;    // workgroup 0, thread 0: the call's receive
+                                        // count and digest (finish_last writes them)
 
     __device__ void preload_ll(long long n) {
 #pragma unroll
@@ -825,8 +827,8 @@ struct Loop {
         }
         const u64 s = a.check ? block_sum(part, lds4) : 0;
         if (threadIdx.x == 0) {
-            __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&a.status->recv_digest, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            rdone = done;
+            rdig = s;
         }
     }
 
@@ -900,6 +902,7 @@ struct Loop {
     // early where they can (the last receive of a side that only waits for
     // it, see k_xfer), so their count is usually in before workgroup 0 looks.
     __device__ bool last_to_finish() const {
+        drain_stores();    // every wave: its stores of the call (rx unpacks, poison) are in memory
         __syncthreads();
         if (gridDim.x == 1) return true;   // (no counter round trip for a 1-workgroup grid)
         if (blockIdx.x != 0) {
@@ -913,23 +916,28 @@ struct Loop {
         __syncthreads();
         return true;
     }
-    // Workgroup 0, last: scratch words [0..3] back to zero for the rank's
-    // next call (so no memset precedes a launch), the call's phase stamps and
-    // exit time, then — after every status store of the call has drained —
-    // the completion word the host spins on (Status.done = this call's token).
+    // Workgroup 0, last (every store of the call has drained: last_to_finish):
+    // the call's end line (Status.fin: receive count and digest, phase stamps,
+    // exit time, the sealed completion word) in ONE store of eight lanes of
+    // wave 0, then scratch words [0..3] back to zero for the rank's next call
+    // (so no memset precedes a launch; the next call's kernel starts only
+    // after this one has retired).
     __device__ void finish_last() const {
-        if (threadIdx.x != 0) return;
+        if (threadIdx.x >= 64) return;
         const u64 t_end = now_ticks();
-        for (int k = 0; k < 4; ++k) __hip_atomic_store(&a.gbar[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.gbar[kScrGo], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.gbar[kScrReady], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        st_sys(&a.status->t_entry, ts[kTsEntry]);
-        st_sys(&a.status->t_posted, ts[kTsPosted]);
-        st_sys(&a.status->t_first, ts[kTsFirst]);
-        st_sys(&a.status->t_loop, ts[kTsLoop]);
-        st_sys(&a.status->t_exit, t_end);
-        drain_stores();
-        st_sys(&a.status->done, a.done_token);
+        const u64 v0 = __shfl(rdone, 0, 64), v1 = __shfl(rdig, 0, 64), v2 = __shfl(ts[kTsEntry], 0, 64),
+                  v3 = __shfl(ts[kTsPosted], 0, 64), v4 = __shfl(ts[kTsFirst], 0, 64), v5 = __shfl(ts[kTsLoop], 0, 64),
+                  v6 = __shfl(t_end, 0, 64);
+        const u64 w = fin_word(a.done_token, v0, v1, v2, v3, v4, v5, v6);
+        const int l = (int)threadIdx.x;
+        const u64 mine = l == 0 ? v0 : l == 1 ? v1 : l == 2 ? v2 : l == 3 ? v3 : l == 4 ? v4 : l == 5 ? v5
+                                                                                         : l == 6 ? v6 : w;
+        if (l < 8) st_sys(&a.status->fin.recv_done + l, mine);
+        if (l == 0) {
+            for (int k = 0; k < 4; ++k) __hip_atomic_store(&a.gbar[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.gbar[kScrGo], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.gbar[kScrReady], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 
     // ---- non-blocking check mode (k_xfer_nbcheck) ----------------------------
@@ -1277,8 +1285,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer(XferArgs a) {
     if constexpr (MODE == MPX_MODE_NONBLOCKING) {
         if (inflight > 0 && !L.aborted() && L.wait_bulk(rxs + a.iters, a.iters - 1))   // final Waitall(inflight)
             done += (u64)inflight;
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (blockIdx.x == 0 && threadIdx.x == 0) L.rdone = done;
         if (L.last_to_finish()) L.finish_last();
     } else if (L.last_to_finish()) {
         L.account(done, (MODE == MPX_MODE_UNIDIR && GROUP == 1) ? 1 : n);
@@ -1348,8 +1355,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_nbcheck(XferArgs a) {
     // every payload: also the receives the reference leaves pending
     if (ok) L.nb_wait([&] { return next >= a.iters; }, &next, a.iters - 1);
     if (w == 0 && threadIdx.x == 0) {
-        __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.status->recv_digest, dig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        L.rdone = done;
+        L.rdig = dig;
     }
     if (L.last_to_finish()) L.finish_last();
 }
@@ -1453,8 +1460,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_xfer_pull(XferArgs a) {
             }
             const u64 s = block_sum(part, lds4);
             if (threadIdx.x == 0) {
-                __hip_atomic_store(&a.status->recv_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&a.status->recv_digest, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                L.rdone = done;
+                L.rdig = s;
             }
         }
         if (L.last_to_finish()) L.finish_last();

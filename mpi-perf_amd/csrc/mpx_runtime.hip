@@ -605,6 +605,28 @@ struct KernelCall {
 // in memory before it is stored; the stream is polled every 50 us so that a
 // kernel that ended without storing it (it cannot, but a fault could) ends
 // the wait with an error instead of a hang.
+// The call's end line (Status.fin) is complete and sealed for `token`: its
+// word carries the token and the seal of the other seven words as read now
+// (a line seen half-written does not match; the caller reads it again).
+bool fin_sealed(const Rank& me, u64 token, Fin* out) {
+    const volatile Fin* f = &me.status->fin;
+    const u64 w = __atomic_load_n(&me.status->fin.word, __ATOMIC_ACQUIRE);
+    if ((w & 0xffffffffull) != (token & 0xffffffffull)) return false;
+    Fin v;
+    v.recv_done = f->recv_done;
+    v.recv_digest = f->recv_digest;
+    v.t_entry = f->t_entry;
+    v.t_posted = f->t_posted;
+    v.t_first = f->t_first;
+    v.t_loop = f->t_loop;
+    v.t_exit = f->t_exit;
+    v.word = w;
+    if (fin_word(token, v.recv_done, v.recv_digest, v.t_entry, v.t_posted, v.t_first, v.t_loop, v.t_exit) != w)
+        return false;
+    if (out) *out = v;
+    return true;
+}
+
 int wait_kernel(Rank& me, u64 token, bool armed, double* t_done) {
     *t_done = 0;
     if (!armed && sync_mode() == kSyncEvent) {
@@ -616,15 +638,15 @@ int wait_kernel(Rank& me, u64 token, bool armed, double* t_done) {
     // back (unarmed) or not at all (armed).
     double next_query = now_s() + 50e-6;
     for (;;) {
-        if (*t_done == 0 && __atomic_load_n(&me.status->done, __ATOMIC_ACQUIRE) == token) {
+        if (*t_done == 0 && fin_sealed(me, token, nullptr)) {
             *t_done = now_s();
             if (armed) return MPX_OK;
         }
         if (*t_done != 0 || now_s() >= next_query) {
             const hipError_t q = armed ? hipStreamQuery(me.stream) : hipEventQuery(me.ev1);
             if (q == hipSuccess) {
-                if (armed && __atomic_load_n(&me.status->done, __ATOMIC_ACQUIRE) != token)
-                    return fail(MPX_ERR_HIP, "armed transfer kernel ended without its completion word");
+                if (armed && !fin_sealed(me, token, nullptr))
+                    return fail(MPX_ERR_HIP, "armed transfer kernel ended without its completion line");
                 if (*t_done == 0) *t_done = now_s();
                 return MPX_OK;
             }
@@ -756,10 +778,7 @@ int launch_call(Rank& me, KernelCall& kc, bool armed) {
     }
     me.status->err = 0;
     me.status->where = 0;
-    me.status->recv_done = 0;
-    me.status->recv_digest = 0;
-    me.status->t_entry = me.status->t_posted = me.status->t_exit = 0;
-    me.status->t_first = me.status->t_loop = 0;
+    memset(&me.status->fin, 0, sizeof(Fin));
     if (armed) {
         __atomic_store_n(&me.status->ready, 0ull, __ATOMIC_RELAXED);
         a.go_token = a.done_token;
@@ -784,9 +803,13 @@ int complete_call(Rank& me, KernelCall& kc, bool armed, double t_call, double t0
     TRY(wait_kernel(me, a.done_token, armed, &t_done));
     const double t_end = now_s();
     t->wall_s = t_end - t0;
-    const u64 te = __atomic_load_n(&me.status->t_entry, __ATOMIC_ACQUIRE);
-    const u64 tp = __atomic_load_n(&me.status->t_posted, __ATOMIC_ACQUIRE);
-    const u64 tx = __atomic_load_n(&me.status->t_exit, __ATOMIC_ACQUIRE);
+    // the end line: sealed once wait_kernel returns (a retired kernel wrote
+    // it whole); a line that does not match here is a kernel that never
+    // wrote it (a fault) and fails the call
+    Fin fin{};
+    if (!fin_sealed(me, a.done_token, &fin))
+        return fail(MPX_ERR_HIP, "rank %d: the transfer kernel left no completion line", kc.my_rank);
+    const u64 te = fin.t_entry, tp = fin.t_posted, tx = fin.t_exit;
     const double kernel_s = (te && tx >= te) ? (double)(tx - te) * 1e-8 : 0;
     if (armed) {
         t->device_s = kernel_s;   // from go seen to the last workgroup's end (s_memrealtime)
@@ -798,8 +821,8 @@ int complete_call(Rank& me, KernelCall& kc, bool armed, double t_call, double t0
     t->launches = 1;
     t->nwg = kc.ll ? 1 : a.nwg;
     t->protocol = kc.ll ? kProtoLL : a.pull ? kProtoPull : kProtoBulk;
-    t->recv_done = __atomic_load_n(&me.status->recv_done, __ATOMIC_ACQUIRE);
-    t->recv_digest = __atomic_load_n(&me.status->recv_digest, __ATOMIC_ACQUIRE);
+    t->recv_done = fin.recv_done;
+    t->recv_digest = fin.recv_digest;
     // phases (mpx_last_phases): the kernel's own clock splits its span; the
     // host's clock brackets it (launch or go before, completion after)
     mpx_phases& ph = me.phases;
@@ -816,8 +839,7 @@ int complete_call(Rank& me, KernelCall& kc, bool armed, double t_call, double t0
     ph.resident = (armed && kc.resident) ? 1 : 0;
     // inside the kernel (k_xfer): the first iteration from the moment this
     // side could start it, and the end after the loop
-    const u64 tf = __atomic_load_n(&me.status->t_first, __ATOMIC_ACQUIRE);
-    const u64 tl = __atomic_load_n(&me.status->t_loop, __ATOMIC_ACQUIRE);
+    const u64 tf = fin.t_first, tl = fin.t_loop;
     const u64 t_go = tp >= te ? tp : te;
     ph.first_iter_s = (te && tf >= t_go) ? (double)(tf - t_go) * 1e-8 : 0;
     ph.tail_s = (tl && tx >= tl) ? (double)(tx - tl) * 1e-8 : 0;
