@@ -905,14 +905,23 @@ struct Loop {
         drain_stores();    // every wave: its stores of the call (rx unpacks, poison) are in memory
         __syncthreads();
         if (gridDim.x == 1) return true;   // (no counter round trip for a 1-workgroup grid)
+        // What workgroup 0 needs from the others is in memory once their
+        // waves have drained (above): their payload, poison and rx stores
+        // are write-through (sc0 sc1) and their checksums atomics.  So the
+        // count is a relaxed add after the drain — an agent-scope release
+        // would add an L2 write-back (buffer_wbl2) with nothing to write —
+        // and workgroup 0 polls it with relaxed loads and invalidates (one
+        // acquire) once, not on every poll.
         if (blockIdx.x != 0) {
             if (threadIdx.x == 0)
-                __hip_atomic_fetch_add(&a.gbar[kScrFin], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&a.gbar[kScrFin], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
-        if (threadIdx.x == 0)
-            while (__hip_atomic_load(&a.gbar[kScrFin], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != (u64)gridDim.x - 1)
+        if (threadIdx.x == 0) {
+            while (__hip_atomic_load(&a.gbar[kScrFin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (u64)gridDim.x - 1)
                 __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
         __syncthreads();
         return true;
     }
