@@ -4,10 +4,16 @@ CPU-only: no compute call is made (argument validation that returns before
 touching the GPU is allowed).
 """
 import ctypes
+import ctypes as C
 import os
+import shutil
 import subprocess
 
+import pytest
+
 import mpx
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_library_built_in_tree():
@@ -76,3 +82,32 @@ def test_header_constants_match_binding():
     assert f"#define MPX_ABI_VERSION {mpx.ABI_VERSION}" in txt
     assert f"#define MPX_XFER_STREAM {mpx.XFER_STREAM}" in txt
     assert f"#define MPX_XFER_PULL {mpx.XFER_PULL}" in txt and mpx.PROTOCOLS[7] == "pull"
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """Every C struct the binding mirrors (mpx_timing, mpx_xfer_opts,
+    mpx_phases) has the binding's size and field offsets: a C program built
+    against include/mpx.h prints them (no GPU, no libmpx call)."""
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    mirrors = {"mpx_timing": mpx.Timing, "mpx_xfer_opts": mpx.XferOpts, "mpx_phases": mpx.Phases}
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "mpx.h"', "int main(void) {"]
+    for cname, py in mirrors.items():
+        src.append(f'    printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            src.append(f'    printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    src += ["    return 0;", "}"]
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src) + "\n")
+    exe = tmp_path / "layout"
+    inc = os.path.join(ROOT, "include")
+    subprocess.run([cc, "-std=c11", "-I", inc, str(c), "-o", str(exe)], check=True, capture_output=True)
+    got = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        name, field, val = line.split()
+        got[(name, field)] = int(val)
+    for cname, py in mirrors.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
