@@ -329,15 +329,32 @@ def loopback_pair(mpx, engine: str, mode: int, nbytes: int, iters: int, runs: in
 POST_TIMEOUT_MS = 2000
 
 
-def safe_wall(c, errs: list, *xfer_args, **xfer_kw) -> float:
+def start_after_barrier(dist, c, *xfer_args, **xfer_kw):
+    """The barrier in front of a timed loop (mpi_perf.c:499), then the
+    transfer.  With the spin barrier (SpinBarrierDist) both happen in one C
+    call (mpxb_spin_wait_xfer): an armed call starts as the barrier opens,
+    with no Python between them — several microseconds that differ from rank
+    to rank and showed up as the sender's wait for its peer's start (the
+    posted wait).  Otherwise dist.barrier(), then the call."""
+    spin = getattr(dist, "spin", None)
+    if spin is not None:
+        return c.xfer(*xfer_args, after=spin, **xfer_kw)
+    dist.barrier()
+    return c.xfer(*xfer_args, **xfer_kw)
+
+
+def safe_wall(c, errs: list, *xfer_args, barrier=None, **xfer_kw) -> float:
     """Wall time of one transfer measured after the headline (latency,
     sweeps); a failure there (a device deadline, a refused transfer, a
     payload checksum mismatch) is recorded in `errs` and returns +inf, so
     this rank still takes part in every collective that follows and the
-    headline line is still printed."""
+    headline line is still printed.  barrier: a dist whose barrier goes in
+    front of the transfer (start_after_barrier)."""
     try:
         # a 2 s per-wait deadline (the longest wait here is one 4 MiB push):
         # a broken link costs each later partner 2 s, not the default 10
+        if barrier is not None:
+            return start_after_barrier(barrier, c, *xfer_args, timeout_ms=POST_TIMEOUT_MS, **xfer_kw).wall_s
         return c.xfer(*xfer_args, timeout_ms=POST_TIMEOUT_MS, **xfer_kw).wall_s
     except Exception as e:  # noqa: BLE001
         errs.append(f"{type(e).__name__}: {e}"[:240])
@@ -383,8 +400,7 @@ def round0_sweep(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, errs) -> dic
 
     def timed(mode, n, it):
         arm(c, errs, mode, g, rank, peer, it, tx, rx, n, timeout_ms=POST_TIMEOUT_MS)
-        dist.barrier()
-        w = torch.tensor([safe_wall(c, errs, mode, g, rank, peer, it, tx, rx, n)], dtype=torch.float64)
+        w = torch.tensor([safe_wall(c, errs, mode, g, rank, peer, it, tx, rx, n, barrier=dist)], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         return float(w[0])
 
@@ -578,8 +594,8 @@ def hbv3_rounds(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs, phases: 
         for rd in range(len(rounds)):
             g, peer = round_role(rounds, rd, rank)
             arm(c, errs, mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES, timeout_ms=POST_TIMEOUT_MS)
-            dist.barrier()
-            walls.append(safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES))
+            walls.append(safe_wall(c, errs, mpx.MODE_UNIDIR, g, rank, peer, HBV3_ITERS, tx, rx, HBV3_BYTES,
+                                   barrier=dist))
             if phases and walls[-1] != float("inf"):
                 ph.append((g, c.phases(rank)))
     w = torch.tensor(walls, dtype=torch.float64)
@@ -894,13 +910,16 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         # it (mpx_xfer_arm; a no-op on the SDMA and RCCL engines)
         armed = not step_err and arm(c, step_err, mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg,
                                      stream=stream, **pkw)
-        dist.barrier()                               # MPI_Barrier, mpi_perf.c:499
         if step_err:                                 # keep joining the barriers, transfer nothing
+            dist.barrier()                           # MPI_Barrier, mpi_perf.c:499
             if armed:
                 c.disarm(rank)
             return g, None
         try:
-            return g, c.xfer(mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg, stream=stream, **pkw)
+            # MPI_Barrier (mpi_perf.c:499), then the loop: one C call with
+            # the spin barrier (start_after_barrier)
+            return g, start_after_barrier(dist, c, mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg,
+                                          stream=stream, **pkw)
         except Exception as e:  # noqa: BLE001
             step_err.append(f"rank {rank}: step {s}: {type(e).__name__}: {e}"[:300])
             return g, None
@@ -1037,6 +1056,11 @@ class SpinBarrierDist:
 
     def barrier(self):
         self._spin.wait()
+
+    @property
+    def spin(self):
+        """the spin barrier itself (start_after_barrier waits on it from C)"""
+        return self._spin
 
     def __getattr__(self, k):
         return getattr(self._dist, k)

@@ -395,6 +395,17 @@ int mpxb_spin_wait(mpxb_spin *s, double timeout_s)
     return 0;
 }
 
+int mpxb_spin_wait_xfer(mpxb_spin *s, double timeout_s, mpxb_xfer_fn fn, void *ctx, int mode, int group, int rank,
+                        int peer, int iters, void *tx, void *rx, int len, const void *opts, void *timing,
+                        int *xfer_rc)
+{
+    if (!fn || !xfer_rc) return err("spin barrier: no transfer to start");
+    const int st = mpxb_spin_wait(s, timeout_s);
+    if (st != 0) return st;
+    *xfer_rc = fn(ctx, mode, group, rank, peer, iters, tx, rx, len, opts, timing);
+    return 0;
+}
+
 void mpxb_spin_close(mpxb_spin *s, int unlink_it)
 {
     if (!s) return;

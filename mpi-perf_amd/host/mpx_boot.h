@@ -60,6 +60,19 @@ int mpxb_allreduce_f64(mpxb *b, double v, double *mn, double *mx, double *sum);
 typedef struct mpxb_spin mpxb_spin;
 int mpxb_spin_open(mpxb_spin **out, const char *name, int nranks, int create);
 int mpxb_spin_wait(mpxb_spin *s, double timeout_s);
+/* Wait on the barrier, then call fn(ctx, mode, ..., timing) — libmpx's
+   mpx_xfer_ex, passed by pointer (this library does not link libmpx) — on
+   this thread with nothing in between, and store its return in *xfer_rc.
+   For a host whose barrier and timed call live in an interpreted layer
+   (bench.py): between leaving the barrier and an armed call's start it adds
+   no interpreter round trip (several microseconds, different on every rank),
+   as mpx_perf, all C, adds none.  Returns the barrier's status; fn is not
+   called when the barrier fails. */
+typedef int (*mpxb_xfer_fn)(void *ctx, int mode, int group, int rank, int peer, int iters, void *tx, void *rx,
+                            int len, const void *opts, void *timing);
+int mpxb_spin_wait_xfer(mpxb_spin *s, double timeout_s, mpxb_xfer_fn fn, void *ctx, int mode, int group, int rank,
+                        int peer, int iters, void *tx, void *rx, int len, const void *opts, void *timing,
+                        int *xfer_rc);
 void mpxb_spin_close(mpxb_spin *s, int unlink_it);
 
 const char *mpxb_error(void);

@@ -255,13 +255,19 @@ class Context:
     def xfer(self, mode: int, group: int, my_rank: int, peer_rank: int, iters: int, tx: Buffer, rx: Buffer,
              length: int, check_payload: bool = False, expect: int = 0, expect_ack: int = 0,
              timeout_ms: int = 0, nwg: int = 0, stream: bool = False, pull: bool = False,
-             stage: bool = True) -> Timing:
+             stage: bool = True, after=None) -> Timing:
+        """mpx_xfer_ex.  after: a spin barrier (mpx.spin.SpinBarrier) to wait
+        on first, from C, so the call starts right as the barrier opens"""
         flags = (XFER_STREAM if stream else 0) | (XFER_PULL if pull else 0) | (0 if stage else XFER_NOSTAGE)
         o = XferOpts(check=1 if check_payload else 0, flags=flags, expect_checksum=expect,
                      expect_ack=expect_ack, timeout_ms=timeout_ms, nwg=nwg)
         t = Timing()
-        st = self.L.mpx_xfer_ex(self.h, mode, group, my_rank, peer_rank, iters, C.c_void_p(tx.ptr),
-                                C.c_void_p(rx.ptr), length, C.byref(o), C.byref(t))
+        if after is not None:
+            st = after.wait_then(C.cast(self.L.mpx_xfer_ex, C.c_void_p), self.h, mode, group, my_rank, peer_rank,
+                                 iters, C.c_void_p(tx.ptr), C.c_void_p(rx.ptr), length, C.byref(o), C.byref(t))
+        else:
+            st = self.L.mpx_xfer_ex(self.h, mode, group, my_rank, peer_rank, iters, C.c_void_p(tx.ptr),
+                                    C.c_void_p(rx.ptr), length, C.byref(o), C.byref(t))
         check(st, "mpx_xfer_ex")
         return t
 

@@ -24,6 +24,9 @@ def lib() -> C.CDLL:
         L.mpxb_spin_open.argtypes = [C.POINTER(C.c_void_p), C.c_char_p, C.c_int, C.c_int]
         L.mpxb_spin_wait.restype = C.c_int
         L.mpxb_spin_wait.argtypes = [C.c_void_p, C.c_double]
+        L.mpxb_spin_wait_xfer.restype = C.c_int
+        L.mpxb_spin_wait_xfer.argtypes = [C.c_void_p, C.c_double, C.c_void_p, C.c_void_p] + [C.c_int] * 5 + [
+            C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         L.mpxb_spin_close.restype = None
         L.mpxb_spin_close.argtypes = [C.c_void_p, C.c_int]
         L.mpxb_error.restype = C.c_char_p
@@ -43,6 +46,16 @@ class SpinBarrier:
     def wait(self, timeout_s: float = 180.0) -> None:
         if lib().mpxb_spin_wait(self.h, timeout_s) != 0:
             raise TimeoutError(lib().mpxb_error().decode())
+
+    def wait_then(self, fn, ctx, mode, group, rank, peer, iters, tx, rx, length, opts, timing,
+                  timeout_s: float = 180.0) -> int:
+        """wait, then fn(ctx, ..., opts, timing) from C with nothing in
+        between (mpxb_spin_wait_xfer); fn's return code"""
+        rc = C.c_int(0)
+        if lib().mpxb_spin_wait_xfer(self.h, timeout_s, fn, ctx, mode, group, rank, peer, iters, tx, rx, length,
+                                     opts, timing, C.byref(rc)) != 0:
+            raise TimeoutError(lib().mpxb_error().decode())
+        return rc.value
 
     def close(self) -> None:
         if self.h:

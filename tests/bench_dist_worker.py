@@ -101,7 +101,10 @@ class FakeMpx:
             FakeMpx.log.append(["rccl_init", r, n])
 
         def xfer(self, mode, group, me, peer, iters, tx, rx, n, check_payload=False, expect=0, expect_ack=0,
-                 timeout_ms=0, nwg=0, stream=False, pull=False, stage=True):
+                 timeout_ms=0, nwg=0, stream=False, pull=False, stage=True, after=None):
+            if after is not None:       # the real binding waits on it from C, then starts the call
+                FakeMpx.log.append(["after_barrier", self.engine, mode, me, iters])
+                after.wait()
             if check_payload and self.engine == "kernel" and scenario == "kernel_fails_validation" and rank == 0:
                 raise FakeError("payload checksum mismatch")
             if (scenario == "kernel_step_fails" and self.engine == "kernel" and rank == 1 and mode == 2 and

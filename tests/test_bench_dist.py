@@ -139,6 +139,14 @@ def test_rounds_peers_and_expected_checksums(world, tmp_path):
         assert set(d["res"]["push_vs_pull"]) >= {f"{p}_{m}_GBps" for p in ("push", "pull")
                                                   for m in ("unidir", "nonblocking")}
         assert "extras_errors" not in d["res"], d["res"].get("extras_errors")
+        # the armed loops (here: the warm-up and timed steps) start from C as
+        # the spin barrier opens (start_after_barrier), each right after its arm
+        log = d["log"]
+        at = [i for i, x in enumerate(log) if x[0] == "xfer" and x[1] == "kernel" and not x[8] and x[2] == 2
+              and x[6] == iters][:warmup + steps]
+        assert len(at) == warmup + steps
+        assert all(log[i - 1][0] == "after_barrier" and log[i - 2][0] == "arm" for i in at), [
+            log[i - 2:i + 1] for i in at[:2]]
 
 
 def test_ipc_failure_on_one_rank_falls_back_to_rccl_on_every_rank(tmp_path):

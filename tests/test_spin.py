@@ -89,3 +89,47 @@ def test_rank_count_must_match():
         b.close()
         spin.unlink(name)
     assert not os.path.exists("/dev/shm" + name)
+
+
+def test_wait_then_calls_through_after_every_rank_arrived():
+    """mpxb_spin_wait_xfer: the call starts only once the barrier opens and
+    its return code comes back.  The callee is a C function of the right
+    shape (mpx_xfer_ex with a NULL context: it returns MPX_ERR_INVALID
+    without touching a GPU)."""
+    import ctypes as C
+
+    import mpx
+    name = f"/mpxbar-test-{uuid.uuid4().hex[:12]}"
+    bars = [spin.SpinBarrier(name, 2, True), spin.SpinBarrier(name, 2, False)]
+    spin.unlink(name)
+    fn = C.cast(mpx.lib().mpx_xfer_ex, C.c_void_p)
+    o, t = mpx.XferOpts(), mpx.Timing()
+    got = []
+
+    def rank(r):
+        got.append(bars[r].wait_then(fn, None, mpx.MODE_UNIDIR, r, r, 1 - r, 1, None, None, 8, C.byref(o),
+                                     C.byref(t), timeout_s=30))
+
+    th = threading.Thread(target=rank, args=(1,))
+    th.start()
+    th.join(0.3)
+    assert th.is_alive() and not got        # rank 1 waits: rank 0 has not arrived
+    rank(0)
+    th.join(30)
+    assert got == [mpx.ERR_INVALID, mpx.ERR_INVALID]
+    for b in bars:
+        b.close()
+
+
+def test_wait_then_times_out_without_calling():
+    import ctypes as C
+
+    import mpx
+    name = f"/mpxbar-test-{uuid.uuid4().hex[:12]}"
+    b = spin.SpinBarrier(name, 2, True)
+    spin.unlink(name)
+    o, t = mpx.XferOpts(), mpx.Timing()
+    with pytest.raises(TimeoutError):
+        b.wait_then(C.cast(mpx.lib().mpx_xfer_ex, C.c_void_p), None, mpx.MODE_UNIDIR, 0, 0, 1, 1, None, None, 8,
+                    C.byref(o), C.byref(t), timeout_s=0.2)
+    b.close()
