@@ -449,11 +449,6 @@ __global__ void k_seqbase(u64* base, u64 tx, u64 rx, int add) {
 // k_xfer: the transfer loop.  One launch runs all `iters` iterations of one
 // rank's side; the peer runs its own launch on its own GPU at the same time.
 // ---------------------------------------------------------------------------
-// armed calls: wave k of a workgroup starts polling for the go k x this
-// s_sleep later (64 clocks per unit: ~0.27 us at 2.4 GHz, about a quarter
-// of a PCIe read round trip)
-constexpr int kGoStagger = 10;
-
 // phase stamps of workgroup 0 (Loop::ts)
 enum { kTsEntry = 0, kTsPosted = 1, kTsFirst = 2, kTsLoop = 3 };
 
@@ -851,59 +846,42 @@ struct Loop {
     // the launch.
     __device__ bool wait_go() const {
         if (!a.go_token) return true;
-        __shared__ int s_go;     // 0 waiting, 1 go, 2 cancelled / no start
-        if (threadIdx.x == 0) s_go = 0;
-        __syncthreads();
-        // Lane 0 of each of the four waves polls, wave k starting k quarter
-        // periods later: a poll is a PCIe (workgroup 0: host memory) or a
-        // memory round trip, so one poller sees the word one to two round
-        // trips after it lands, four staggered ones within about 1.25 —
-        // which also narrows how far apart the two sides of a pair start.
-        // The first to see it tells the others through LDS.
-        const int wave = (int)threadIdx.x >> 6;
-        if ((threadIdx.x & 63) == 0) {
-            if (blockIdx.x != 0 && wave == 0)
-                __hip_atomic_fetch_add(&a.gbar[kScrReady], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int k = 0; k < wave; ++k) __builtin_amdgcn_s_sleep(kGoStagger);
+        __shared__ int s_go;
+        if (threadIdx.x == 0) {
             const u64 t0 = now_ticks();
-            u64 spins = 0;
-            bool told = false;
-            for (;;) {
-                int w = 0;
-                if (blockIdx.x == 0) {
-                    if (wave == 0 && !told &&
-                        __hip_atomic_load(&a.gbar[kScrReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                            (u64)gridDim.x - 1) {
+            u64 spins = 0, w = 0;
+            if (blockIdx.x == 0) {
+                bool told = false;
+                for (;;) {
+                    if (!told && __hip_atomic_load(&a.gbar[kScrReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                     (u64)gridDim.x - 1) {
                         st_sys(&a.status->ready, a.go_token);
                         told = true;
                     }
                     const u64 v = ld_sys(&a.status->go);
-                    w = v == a.go_token ? 1 : v == (a.go_token | kGoCancel) ? 2 : 0;
-                    if (!w && wave == 0 && (++spins & 63) == 0 && now_ticks() - t0 > a.go_timeout_ticks) {
+                    if (v == a.go_token) { w = 1; break; }
+                    if (v == (a.go_token | kGoCancel)) { w = 2; break; }
+                    if ((++spins & 63) == 0 && now_ticks() - t0 > a.go_timeout_ticks) {
                         __hip_atomic_store(&a.status->err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         w = 2;
+                        break;
                     }
-                } else {
-                    // workgroup 0's verdict; (it answers within its own
-                    // deadline: one second more bounds this wait should it
-                    // never run)
-                    w = (int)__hip_atomic_load(&a.gbar[kScrGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (!w && wave == 0 && (++spins & 63) == 0 && now_ticks() - t0 > a.go_timeout_ticks + 100000000ull)
-                        w = 2;
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                if (w) {
-                    __hip_atomic_store(&s_go, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    break;
+                __hip_atomic_store(&a.gbar[kScrGo], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_fetch_add(&a.gbar[kScrReady], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // (workgroup 0 answers within its own deadline; one second
+                // more bounds this wait should it never run)
+                while ((w = __hip_atomic_load(&a.gbar[kScrGo], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                    if ((++spins & 63) == 0 && now_ticks() - t0 > a.go_timeout_ticks + 100000000ull) { w = 2; break; }
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                if (__hip_atomic_load(&s_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                __builtin_amdgcn_s_sleep(2);
             }
+            s_go = (int)w;
         }
         __syncthreads();
-        const int w = s_go;
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            __hip_atomic_store(&a.gbar[kScrGo], (u64)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return w == 1;
+        return s_go == 1;
     }
 
     // ---- call phases and the end of the call --------------------------------
