@@ -6,7 +6,7 @@
 # init when ranks share a GPU: VERDICT r03 next 5b).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04d
+O=gpurun_out/${R04_OUT:-r04d}
 mkdir -p $O
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_self -o x \
     -- python3 -u tools/pmc_xfer.py self nbpull 4096 256 > $O/pmc_self.log 2>&1
