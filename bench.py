@@ -174,13 +174,21 @@ def traffic_from_profile(workload: str) -> dict | None:
         return json.load(f)
 
 
+PROFILER_ENV = ("ROCP_TOOL_LIBRARIES", "ROCPROF_COUNTERS", "ROCPROFILER_LIBRARY_CTOR")
+
+
+def profiled() -> bool:
+    """the process runs under rocprofv3 (its tool library is preloaded)"""
+    return any(os.environ.get(k) for k in PROFILER_ENV)
+
+
 def counters_skip_reason(args) -> str | None:
     """None when the in-process counters may run; else why not.  A process
     that rocprofv3 already profiles has its own rocprofiler tool (and
     dispatch counting serialises kernels): no second one is added."""
     if args.no_counters:
         return "--no-counters"
-    for k in ("ROCP_TOOL_LIBRARIES", "ROCPROF_COUNTERS", "ROCPROFILER_LIBRARY_CTOR"):
+    for k in PROFILER_ENV:
         if os.environ.get(k):
             return f"not sampled in-process: the process runs under a profiler ({k} set)"
     return None
@@ -803,7 +811,7 @@ def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict
 
 
 def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                latency=True, tune=True, pull=False, prof=None) -> dict:
+                latency=True, tune=True, pull=False, prof=None, count: bool = False) -> dict:
     """All-pairs rounds on `engine` (one process per GPU, IPC-mapped peers;
     pull: the engine's MPX_XFER_PULL form, validation and steps alike).
     Every round's payloads are validated once (check mode, seeded per-rank
@@ -967,12 +975,22 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     nw = torch.tensor([float(step_nwg)], dtype=torch.float64)
     dist.all_reduce(nw, op=dist.ReduceOp.MAX)
     out["push_nwg"] = int(nw[0])
-    if prof is not None and engine == "kernel":
-        errs = []
-        out["counters"] = link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes, iters, nwg,
-                                        stream, [d[3] for d in descs], errs)
-        if errs:
-            out["counters"]["transfer_errors"] = errs[:3]
+    if count and engine == "kernel":
+        # every rank joins the passes' rounds; the sampling ranks (the lowest
+        # on each bus id) must hold the tool, or no rank runs them
+        buses = [d[3] for d in descs]
+        samplers = [r for r in range(world) if r == min(q for q in range(world) if buses[q] == buses[r])]
+        have = [None] * world
+        dist.all_gather_object(have, prof is not None)
+        missing = [r for r in samplers if not have[r]]
+        if missing:
+            out["counters"] = {"error": f"the counter tool is not running on sampling rank(s) {missing}"}
+        else:
+            errs = []
+            out["counters"] = link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes, iters,
+                                            nwg, stream, buses, errs)
+            if errs:
+                out["counters"]["transfer_errors"] = errs[:3]
     ll_old = os.environ.get("MPX_LL_MAX")
     if latency:
         # after the headline: a failure here costs its own numbers only
@@ -1018,13 +1036,13 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
 
 
 def pairs_with_fallback(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                        extras: dict, latency: bool = True, prof=None) -> tuple[dict, str]:
+                        extras: dict, latency: bool = True, prof=None, count: bool = False) -> tuple[dict, str]:
     """pairs_bench on `engine`; if the kernel engine fails (payload
     validation, or a device timeout on any rank in validation or in the timed
     steps), measure the SDMA engine instead and say so: an explicit, labelled
     fallback, never a silent one."""
     res = pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps, warmup, barrier_sync,
-                      latency=latency, prof=prof)
+                      latency=latency, prof=prof, count=count)
     engine_used = engine
     if res.get("error") and engine == "kernel":
         extras["kernel_engine_error"] = res["error"]
@@ -1158,6 +1176,12 @@ def main() -> None:
     # In-process counters (roofline.traffic): the tool registers before the
     # first HIP call of this process (torch is imported, HIP not started yet)
     prof, prof_note = None, counters_skip_reason(args)
+    count = prof_note is None            # alike on every rank (arguments and environment)
+    if count and os.environ.get("MPX_BENCH_ONE_GPU") and world > 1 and rank != 0:
+        # one-GPU rehearsal: rank 0 samples the shared card; the tool in
+        # every process added a queue per process to a card whose queue slots
+        # the rehearsal already fills (N = 8 ran ~5x slower with it)
+        prof_note = "one-GPU rehearsal: rank 0 samples the card"
     if prof_note is None:
         try:
             counters.register()
@@ -1265,7 +1289,7 @@ def main() -> None:
         # the timed launches as the last ones)
         res, engine_used = pairs_with_fallback(mpx, torch, pdist, args.engine, rank, world, dev, nbytes, iters,
                                                args.steps, args.warmup, barrier_sync, extras,
-                                               latency=not args.no_extras, prof=prof)
+                                               latency=not args.no_extras, prof=prof, count=count)
         elapsed, total = res["elapsed"], res["total"]
         achieved = res["per_pair_GBps"]
         roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",
@@ -1449,9 +1473,15 @@ def main() -> None:
     # faulted inside rocprofiler-sdk's finalizer while rank streams were
     # alive (profiles/r04_exit_segv_stack.txt), and destroying them first
     # (mpx_shutdown) stalled 1 processes-mode exit in 4 inside the runtime
-    # (profiles/r04_procs_exit_stall.txt).
+    # (profiles/r04_procs_exit_stall.txt).  Under a profiler the normal
+    # exit stays: rocprofv3 writes its output from its own exit-time
+    # finalizer, so the rank streams are destroyed first (mpx_shutdown, the
+    # one-process order that exits 0: counters_probe, tools/pmc_xfer.py).
     sys.stdout.flush()
     sys.stderr.flush()
+    if profiled():
+        mpx.shutdown()
+        return
     os._exit(0)
 
 

@@ -197,12 +197,16 @@ if __name__ == "__main__":
             out.update(res=bench.pairs_bench(FakeMpx, torch, dist, "rccl", rank, world, 0, nbytes, 7, 5, 2,
                                              dist.barrier, latency=False))
         else:
-            prof = FakeProf if scenario in ("counters", "one_gpu") else None
+            # one_gpu: only rank 0 registers the tool (bench.main's one-GPU
+            # rehearsal); counters_missing: sampling rank 1 has none
+            prof = FakeProf if (scenario == "counters" or (scenario == "one_gpu" and rank == 0)
+                                or (scenario == "counters_missing" and rank != 1)) else None
+            count = scenario in ("counters", "one_gpu", "counters_missing")
             # the per-round barriers spin in shared memory, as in bench.main (world 2 and 4 here)
             d, spin = bench.spin_barrier_dist(dist, rank, world) if scenario == "ok" else (dist, None)
             out["spin"] = spin is not None
             res, used = bench.pairs_with_fallback(FakeMpx, torch, d, "kernel", rank, world, 0, nbytes, 7, 5, 2,
-                                                  dist.barrier, extras, prof=prof)
+                                                  dist.barrier, extras, prof=prof, count=count)
             out.update(res=res, engine_used=used, extras=extras, passes=FakeProf.passes)
     except SystemExit as e:
         out.update(exit=str(e))

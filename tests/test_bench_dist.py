@@ -274,6 +274,17 @@ def test_link_counters_one_sampler_per_gpu(world, scenario, tmp_path):
                                                         for x in inside)
 
 
+def test_link_counters_need_the_tool_on_every_sampling_rank(tmp_path):
+    """A sampling rank without the counter tool (its registration failed):
+    every rank skips the passes alike (no rank left inside a collective the
+    others never enter) and the line says which rank lacked it."""
+    res = run(4, "counters_missing", tmp_path)
+    for d in res:
+        assert d["res"]["counters"] == {"error": "the counter tool is not running on sampling rank(s) [1]"}
+        assert not d["passes"]
+        assert "error" not in d["res"] or d["res"].get("counters")
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_cpu_baseline_beside_the_pairs_line(world):
     """The reference itself beside the N >= 2 line:
