@@ -1176,12 +1176,17 @@ def main() -> None:
     # In-process counters (roofline.traffic): the tool registers before the
     # first HIP call of this process (torch is imported, HIP not started yet)
     prof, prof_note = None, counters_skip_reason(args)
+    if prof_note is None and os.environ.get("MPX_BENCH_ONE_GPU") and world > 2:
+        # One-GPU rehearsal beyond a single pair: not sampled.  The device
+        # counting service reads the counters of ITS process's work here
+        # (rank 0 alone read 0.25 x the card's pushes at N = 8 = its own
+        # share, profiles/r04_bench_n8_onegpu_rehearsal_rank0_tool.json), and
+        # the tool in every process cost the card's shared queue slots a 5x
+        # slowdown (r04_bench_n8_onegpu_rehearsal_tool_everywhere.json).  On
+        # a node, each GPU's one process is its sampler; at N = 2 here the
+        # sampler (rank 0) is the side that pushes.
+        prof_note = "one-GPU rehearsal with more than one pair: not sampled (per-process counters, shared queues)"
     count = prof_note is None            # alike on every rank (arguments and environment)
-    if count and os.environ.get("MPX_BENCH_ONE_GPU") and world > 1 and rank != 0:
-        # one-GPU rehearsal: rank 0 samples the shared card; the tool in
-        # every process added a queue per process to a card whose queue slots
-        # the rehearsal already fills (N = 8 ran ~5x slower with it)
-        prof_note = "one-GPU rehearsal: rank 0 samples the card"
     if prof_note is None:
         try:
             counters.register()
