@@ -9,7 +9,9 @@ mode every payload is checksummed on the device.
     python tools/soak.py procs <calls> <seed> [engine]     two processes over IPC
     python tools/soak.py worker <dir> <rank> <calls> <seed> <engine>   (one process of `procs`)
 
-engine: kernel (default) or sdma; both with push and pull calls.  With a
+engine: kernel (default) or sdma; both with push and pull calls; half of the
+calls armed (mpx_xfer_arm before the call; one in ten of those cancelled
+with mpx_xfer_disarm and run unarmed).  With a
 negative-control knob set (MPX_TEST=no_posted, MPX_TEST=no_pull_wait) the
 soak must report failures: that is what shows it can see the races.
 
@@ -45,9 +47,14 @@ def plan(calls, seed, engine="kernel"):
         else:
             iters = rng.randint(1, 40) if n <= (1 << 20) else rng.randint(1, 8)
         pull = rng.random() < 0.5
-        out.append(dict(mode=mode, n=n, iters=iters, check=rng.random() < 0.6, pull=pull,
-                        nwg=rng.choice([0, 0, 1, 3, 8, 64, 128, 256]), stream=rng.random() < 0.3,
-                        refill=rng.random() < 0.2, key=rng.getrandbits(32)))
+        step = dict(mode=mode, n=n, iters=iters, check=rng.random() < 0.6, pull=pull,
+                    nwg=rng.choice([0, 0, 1, 3, 8, 64, 128, 256]), stream=rng.random() < 0.3,
+                    refill=rng.random() < 0.2, key=rng.getrandbits(32))
+        # armed calls (mpx_xfer_arm, then the same call starts it), a few of
+        # them cancelled first (mpx_xfer_disarm, then the call runs unarmed)
+        step["armed"] = rng.random() < 0.5
+        step["cancel"] = step["armed"] and rng.random() < 0.1
+        out.append(step)
     return out
 
 
@@ -60,10 +67,14 @@ def run_rank(c, rank, tx, rx, steps, peer_sum):
         if s["refill"]:
             c.fill(tx, CAP, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, rank, peer, s["key"] & 0xFFFF))
         m = 1 if (s["mode"] == mpx.MODE_UNIDIR and group == 1) else s["n"]
+        kw = dict(check_payload=s["check"], expect=peer_sum(k, s["n"]), expect_ack=peer_sum(k, 1), timeout_ms=10000,
+                  nwg=s["nwg"], stream=s["stream"], pull=s["pull"])
         try:
-            t = c.xfer(s["mode"], group, rank, peer, s["iters"], tx, rx, s["n"], check_payload=s["check"],
-                       expect=peer_sum(k, s["n"]), expect_ack=peer_sum(k, 1), timeout_ms=10000, nwg=s["nwg"],
-                       stream=s["stream"], pull=s["pull"])
+            if s.get("armed"):
+                c.arm(s["mode"], group, rank, peer, s["iters"], tx, rx, s["n"], **kw)
+                if s.get("cancel"):
+                    c.disarm(rank)
+            t = c.xfer(s["mode"], group, rank, peer, s["iters"], tx, rx, s["n"], **kw)
             if s["check"] and (t.check_failures or t.check_iters != s["iters"]):
                 fails.append(dict(call=k, step=s, what="check", t=t.as_dict()))
             if c.checksum(rx, m) != peer_sum(k, m):
