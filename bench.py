@@ -1325,9 +1325,7 @@ def main() -> None:
                       barrier=("node-local spin barrier in shared memory before every loop (mpx/spin.py)"
                                if spin is not None else "gloo"),
                       launch=("armed: each loop's kernel launched before its barrier, started by a host-memory "
-                              "word after it (mpx_xfer_arm); its receives are posted when the kernel runs, before "
-                              "the barrier (no byte moves before the start)" if engine_used == "kernel"
-                              else "inline"),
+                              "word after it (mpx_xfer_arm)" if engine_used == "kernel" else "inline"),
                       # bytes of tx each pushing workgroup holds in LDS (read once per call; 0 = tx read from HBM)
                       stage=chunk if (engine_used == "kernel" and 0 < chunk <= 60 << 10) else 0)
         if "ll_max" in res:

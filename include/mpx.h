@@ -255,11 +255,7 @@ int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank
    part of every short loop's recorded time.  The armed call's device_s is
    the kernel's own clock from start to end.  mpx_xfer_arm returns once the
    kernel's whole grid runs and waits (at most 5 ms later), so the start does
-   not also pay the rest of the dispatch.  The armed call's receives are
-   posted when its kernel runs: from mpx_xfer_arm on, rx belongs to the call
-   (the peer's pushes of this call may land before this rank's start, as they
-   could into a receive posted before the barrier); a host reads rx before it
-   arms, not between arm and start.  A rank holds one armed call;
+   not also pay the rest of the dispatch.  A rank holds one armed call;
    mpx_xfer_ex with other arguments fails (MPX_ERR_STATE) and leaves it
    armed.  The SDMA and RCCL engines accept the call and do nothing. */
 int mpx_xfer_arm(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,

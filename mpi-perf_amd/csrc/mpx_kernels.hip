@@ -846,13 +846,6 @@ struct Loop {
     // the launch.
     __device__ bool wait_go() const {
         if (!a.go_token) return true;
-        // An armed call's receives are posted as soon as its kernel runs
-        // (the previous call on this stream has retired, and the host handed
-        // rx to the call when it armed it): the peer's first push of the
-        // call need not wait for this side's start after the barrier, as a
-        // receive posted before MPI_Barrier would not make it wait.  The
-        // call posts the same number again after the go (idempotent).
-        post_receives();
         __shared__ int s_go;
         if (threadIdx.x == 0) {
             const u64 t0 = now_ticks();
