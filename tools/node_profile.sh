@@ -26,10 +26,9 @@ N=${N:-2}
 O=gpurun_out/node_prof_n$N
 mkdir -p $O
 export TMPDIR=/tmp WORLD_SIZE=$N MASTER_ADDR=127.0.0.1
-# round 2's exit order (drain, 50 ms, destroy the pooled streams in libmpx's
-# exit handler, before the profiler's): under rocprofv3 --pmc the default
-# (streams left to the runtime's teardown) segfaults in __cxa_finalize after
-# the profiler wrote its output (tools/gpu_pmc_pull.sh, round 3)
+# Under rocprofv3 bench.py destroys its rank streams (mpx_shutdown) and exits
+# normally, so the profiler's exit-time finalizer writes the output and finds
+# no live CU-masked queue (profiles/r04_exit_segv_stack.txt)
 STEPS=${STEPS:-$((2 * (N - 1)))}
 run_pass() {   # pass-name, rocprofv3 options...
     local pass=$1; shift
