@@ -1088,7 +1088,11 @@ def spin_barrier_dist(dist, rank: int, world: int):
     """(SpinBarrierDist, spin) when every rank opened the shm barrier, else
     (dist, None): every rank decides alike."""
     from mpx import spin as sp
-    name = f"/mpxbar-bench-{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}"
+    # one name per job on this node: its rendezvous address, port and size
+    # (ranks started by hand, as tools/node_profile.sh does, have different
+    # parents, so the launcher's pid cannot name it)
+    name = "/mpxbar-bench-{}-{}-{}".format(os.environ.get("MASTER_ADDR", "x").replace("/", "_"),
+                                           os.environ.get("MASTER_PORT", "0"), world)
     s, err = None, ""
     try:
         if rank == 0:
@@ -1186,7 +1190,7 @@ def main() -> None:
         # a node, each GPU's one process is its sampler; at N = 2 here the
         # sampler (rank 0) is the side that pushes.
         prof_note = "one-GPU rehearsal with more than one pair: not sampled (per-process counters, shared queues)"
-    count = prof_note is None            # alike on every rank (arguments and environment)
+    count = prof_note is None            # agreed across ranks below (environments may differ)
     if prof_note is None:
         try:
             counters.register()
@@ -1215,6 +1219,14 @@ def main() -> None:
         import torch.distributed as dist
         # a rank that dies must not leave the others in a 30-minute gloo wait
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=180))
+        # the counter passes need every rank (they re-run every round): only
+        # when every rank can take part — ranks started by hand may differ,
+        # e.g. tools/node_profile.sh runs some under rocprofv3 and some not
+        flags = [None] * world
+        dist.all_gather_object(flags, count)
+        if count and not all(flags):
+            prof_note = "not sampled: another rank runs without the in-process counters (under a profiler or --no-counters)"
+        count = all(flags)
 
     def barrier_sync():
         torch.cuda.synchronize()
