@@ -1,6 +1,10 @@
 #!/bin/bash
 # one-workgroup waits: one polling wave (stagger 0) vs four staggered waves
-# (6, 12 s_sleep units), interleaved twice, then the engine tests on the default
+# (6, 12 s_sleep units), interleaved twice, then the engine tests on the default.
+# The variants were built on the CPU from the staggered-wait revision of
+# csrc/mpx_kernels.hip (git history: "A/B of staggered polling waves"), with
+# -DMPX_POLL_STAGGER=N, into mpi-perf_amd/lib/variants/libmpx_staggerN.so;
+# that revision was not kept, so rebuild them from it before re-running.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/poll_stagger
