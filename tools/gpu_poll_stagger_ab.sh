@@ -1,10 +1,12 @@
 #!/bin/bash
 # one-workgroup waits: one polling wave (stagger 0) vs four staggered waves
 # (6, 12 s_sleep units), interleaved twice, then the engine tests on the default.
-# The variants were built on the CPU from the staggered-wait revision of
-# csrc/mpx_kernels.hip (git history: "A/B of staggered polling waves"), with
-# -DMPX_POLL_STAGGER=N, into mpi-perf_amd/lib/variants/libmpx_staggerN.so;
-# that revision was not kept, so rebuild them from it before re-running.
+# The variants were built on the CPU from an uncommitted experiment on
+# csrc/mpx_kernels.hip (four waves polling in wait_ll / wait_bulk of a
+# one-workgroup grid, wave k starting k x MPX_POLL_STAGGER s_sleep units
+# later, the first to see the message claiming it through LDS), with
+# -DMPX_POLL_STAGGER=N, into mpi-perf_amd/lib/variants/libmpx_staggerN.so.
+# It lost the A/B (profiles/r04_poll_stagger_ab.jsonl) and was not kept.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/poll_stagger
