@@ -13,7 +13,7 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "extras"}
 
 
-def run(scenario, world=2):
+def run(scenario, world=2, extra_env=None):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -21,7 +21,7 @@ def run(scenario, world=2):
     ps = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", **(extra_env or {}))
         ps.append(subprocess.Popen([sys.executable, os.path.join(HERE, "bench_main_worker.py"), scenario, "--gpus",
                                     str(world), "--steps", "3", "--warmup", "1"], stdout=subprocess.PIPE,
                                    stderr=subprocess.PIPE, text=True, env=env))
@@ -67,6 +67,23 @@ def test_one_json_line_with_the_contract_keys():
     assert d["extras"]["unidir_4MiB_unstaged_GBps"] is not None
     assert d["extras"]["hbv3_rounds_unidir"]["phases_us_median"]["g1"]["kernel_s"] == 1.0
     assert d["config"]["barrier"].startswith("node-local spin barrier") and d["config"]["launch"].startswith("armed")
+
+
+def test_exit_path_with_and_without_a_profiler():
+    """Unprofiled, every rank ends itself after its line (os._exit: no
+    exit-time runtime teardown).  Under rocprofv3 (one of its variables set;
+    ROCPROF_COUNTERS here — the tool-library variable would make the SDK in
+    this process try to load that library) every rank destroys its rank
+    streams (mpx_shutdown) and returns through the normal exit, where the
+    profiler writes its output; the in-process counters stand aside (one
+    rocprofiler tool per process)."""
+    rcs, outs = run("ok")
+    assert rcs == [0, 0] and not any("MAIN_RETURNED" in o[1] for o in outs)
+    rcs, outs = run("ok", extra_env={"ROCPROF_COUNTERS": "FETCH_SIZE"})
+    assert rcs == [0, 0], [o[1][-600:] for o in outs]
+    assert all("MAIN_RETURNED shutdown=True" in o[1] for o in outs), [o[1][-300:] for o in outs]
+    d = lines(outs[0][0])[0]
+    assert d["roofline"]["traffic"] is None and "under a profiler" in d["roofline"]["traffic_source"]
 
 
 def test_hung_comparison_engine_cannot_cost_the_line():
