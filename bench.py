@@ -1315,6 +1315,9 @@ def main() -> None:
                     frac_of_bidirectional_link=round(achieved / XGMI_LINK_PEAK_BIDIR_GBPS, 4),
                     kernel="k_xfer (G1 side)" if engine_used == "kernel" else engine_used,
                     avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
+        if os.environ.get("MPX_BENCH_ONE_GPU"):
+            roof["rehearsal_note"] = ("one-GPU rehearsal: every rank on one card, so achieved is a loopback (HBM) "
+                                      "rate and frac against the link peak says nothing about a link")
         # Link bytes of THIS run's sender launches, read in-process
         # (link_counters): per G1 launch, EA write requests not destined for
         # local DRAM x 64 B.  On the one-GPU rehearsal they are ~0 and the
