@@ -111,3 +111,39 @@ def test_struct_layouts_match_the_header(tmp_path):
         assert got[(cname, "size")] == C.sizeof(py), cname
         for f, _ in py._fields_:
             assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def test_completion_line_layout_and_seal(tmp_path):
+    """The kernel engine's call end (mpx_internal.h Fin): one 64-byte,
+    64-byte-aligned line inside the host-mapped Status (the kernel writes it
+    with a single eight-lane store), and a completion word carrying the
+    call token's low 32 bits and a seal that changes with any other field.
+    Host-only compile of the internal header (no GPU)."""
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no C++ compiler")
+    src = tmp_path / "fin.cpp"
+    src.write_text("""#include "mpx_internal.h"
+#include <cstddef>
+#include <cstdio>
+using namespace mpx;
+int main() {
+    const u64 t = 0x1234567890ull;
+    const u64 w = fin_word(t, 1, 2, 3, 4, 5, 6, 7);
+    int differ = 1;
+    for (int k = 0; k < 7; ++k) {
+        u64 v[7] = {1, 2, 3, 4, 5, 6, 7};
+        v[k] ^= 1;
+        differ &= fin_word(t, v[0], v[1], v[2], v[3], v[4], v[5], v[6]) != w;
+    }
+    printf("%zu %zu %zu %zu %d %d\\n", sizeof(Fin), alignof(Fin), offsetof(Status, fin) % 64,
+           offsetof(Fin, word), (int)((w & 0xffffffffull) == (t & 0xffffffffull)), differ);
+    return 0;
+}
+""")
+    exe = tmp_path / "fin"
+    subprocess.run([cxx, "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I", os.path.join(ROOT, "mpi-perf_amd", "csrc"), str(src), "-o", str(exe)],
+                   check=True, capture_output=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    assert out == ["64", "64", "0", "56", "1", "1"], out
