@@ -177,11 +177,6 @@ def traffic_from_profile(workload: str) -> dict | None:
 PROFILER_ENV = ("ROCP_TOOL_LIBRARIES", "ROCPROF_COUNTERS", "ROCPROFILER_LIBRARY_CTOR")
 
 
-def profiled() -> bool:
-    """the process runs under rocprofv3 (its tool library is preloaded)"""
-    return any(os.environ.get(k) for k in PROFILER_ENV)
-
-
 def counters_skip_reason(args) -> str | None:
     """None when the in-process counters may run; else why not.  A process
     that rocprofv3 already profiles has its own rocprofiler tool (and
@@ -1489,22 +1484,17 @@ def main() -> None:
         if spin is not None:
             spin.close()
         dist.destroy_process_group()
-    # Every context is finalized and the line is out: the process ends here,
-    # without the exit-time teardown of the HIP runtime and of the counter
-    # tool (the driver releases the process's GPU state).  That teardown
-    # faulted inside rocprofiler-sdk's finalizer while rank streams were
-    # alive (profiles/r04_exit_segv_stack.txt), and destroying them first
-    # (mpx_shutdown) stalled 1 processes-mode exit in 4 inside the runtime
-    # (profiles/r04_procs_exit_stall.txt).  Under a profiler the normal
-    # exit stays: rocprofv3 writes its output from its own exit-time
-    # finalizer, so the rank streams are destroyed first (mpx_shutdown, the
-    # one-process order that exits 0: counters_probe, tools/pmc_xfer.py).
+    # Every context is finalized and the line is out: the pooled rank streams
+    # are destroyed here, in the program's own flow, and the process then
+    # ends through its normal exit (the HIP runtime's and any profiler's or
+    # counter tool's exit-time teardown included).  Round 4 ended here with
+    # os._exit(0): the teardown had faulted inside rocprofiler-sdk's
+    # finalizer while rank streams were alive (profiles/r04_exit_segv_stack.txt),
+    # and the destroy had stalled 1 processes-mode exit in 4 — root-caused in
+    # round 5 (DESIGN.md §5 "Exit") and closed by mpx_shutdown's fence.
     sys.stdout.flush()
     sys.stderr.flush()
-    if profiled():
-        mpx.shutdown()
-        return
-    os._exit(0)
+    mpx.shutdown()
 
 
 if __name__ == "__main__":

@@ -10,7 +10,9 @@
 //   mpx_barrier              MPI_Barrier                          :499, :557, :579
 #include "mpx_internal.h"
 
-#include <rccl/rccl.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <rccl/rccl.h>   // types only: the functions are bound at run time (rccl_api)
 
 #include <atomic>
 #include <condition_variable>
@@ -18,6 +20,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include <dlfcn.h>
@@ -50,11 +53,79 @@ int fail(int code, const char* fmt, ...) {
             return fail(MPX_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
     } while (0)
 
+// RCCL is bound at run time from ONE file, the image's /opt/rocm/lib/librccl.so.1
+// (MPX_RCCL_LIB overrides), opened RTLD_LOCAL | RTLD_DEEPBIND: no symbol of it
+// enters the process's global scope, and its own references resolve inside
+// it.  A process that already holds another librccl.so.1 (torch's bundled
+// 2.26.6 in bench.py) therefore cannot shadow it, and bench.py and mpx_perf
+// run the same RCCL.  Linking -lrccl bound libmpx to
+// whichever librccl.so.1 the process had loaded first.
+struct RcclApi {
+    void* h = nullptr;
+    char path[512] = {0};
+    char error[512] = {0};
+    ncclResult_t (*GetVersion)(int*) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+};
+
+const RcclApi& rccl_api() {
+    static const RcclApi* api = [] {
+        RcclApi* a = new RcclApi;   // never destroyed, never dlclosed (exit-time ordering)
+        const char* want = getenv("MPX_RCCL_LIB");
+        if (!want || !*want) want = "/opt/rocm/lib/librccl.so.1";
+        a->h = dlopen(want, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+        if (!a->h) {
+            snprintf(a->error, sizeof a->error, "cannot load %s: %s", want, dlerror());
+            return a;
+        }
+        bool ok = true;
+        auto bind = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(a->h, name));
+            if (!fn && ok) {
+                snprintf(a->error, sizeof a->error, "%s has no %s", want, name);
+                ok = false;
+            }
+        };
+        bind(a->GetVersion, "ncclGetVersion");
+        bind(a->GetErrorString, "ncclGetErrorString");
+        bind(a->GetUniqueId, "ncclGetUniqueId");
+        bind(a->CommInitRank, "ncclCommInitRank");
+        bind(a->CommInitAll, "ncclCommInitAll");
+        bind(a->CommDestroy, "ncclCommDestroy");
+        bind(a->GroupStart, "ncclGroupStart");
+        bind(a->GroupEnd, "ncclGroupEnd");
+        bind(a->Send, "ncclSend");
+        bind(a->Recv, "ncclRecv");
+        if (!ok) {
+            a->h = nullptr;   // unusable: every RCCL entry point fails with the error
+            return a;
+        }
+        Dl_info info{};
+        snprintf(a->path, sizeof a->path, "%s",
+                 dladdr(reinterpret_cast<void*>(a->GetVersion), &info) && info.dli_fname ? info.dli_fname : want);
+        return a;
+    }();
+    return *api;
+}
+
+#define RCCL_LOADED()                                                      \
+    do {                                                                   \
+        if (!rccl_api().h) return fail(MPX_ERR_RCCL, "%s", rccl_api().error); \
+    } while (0)
+
 #define NCCLCK(expr)                                                                                \
     do {                                                                                            \
         ncclResult_t r_ = (expr);                                                                   \
         if (r_ != ncclSuccess)                                                                      \
-            return fail(MPX_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #expr, ncclGetErrorString(r_)); \
+            return fail(MPX_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #expr, rccl_api().GetErrorString(r_)); \
     } while (0)
 
 #define TRY(expr)                     \
@@ -392,22 +463,23 @@ TestKnobs test_knobs() {
 // kernel on such a destroyed stream leaves the runtime waiting on that queue:
 // the next queue creation, stream destruction or the process exit hangs
 // ("a0 m0 k0.0 d0 f0" hangs at exit; "a0 m0 k0.0 f0 d0" is fine; freeing a
-// buffer no kernel touched is fine either way).  Even with every allocation
-// of a context freed before its streams are destroyed, a long-lived process
-// that creates and finalizes contexts one after another stalled in a later
-// context (the -m gpu suite: profiles/r02_stream_destroy_suite_hang.txt,
-// r02_stream_pool_ab.txt) when each destroy followed its drain directly,
-// and still did after a device-wide hipDeviceSynchronize
-// (profiles/r02_stream_destroy_devsync.txt) or after callback_fence
-// (profiles/r03_pytest_nopool.log).  Rank streams are therefore
-// process-lifetime objects, like the runtime's own queues: mpx_finalize
+// buffer no kernel touched is fine either way).  The other stalls of rounds
+// 2-4 — in a later context of the -m gpu suite when each finalize destroyed
+// its streams (profiles/r02_stream_destroy_suite_hang.txt,
+// r03_pytest_nopool.log) and at exit in processes mode
+// (r04_procs_exit_stall.txt) — were one race, root-caused in round 5 from
+// the stacks (profiles/r05_exit_stall_symbolized.txt): the destroy dropped
+// its reference before HIP's completion handler of the stream's last
+// command did, and the queue was then destroyed on the HSA events thread,
+// which deadlocked on itself.  callback_fence now closes it
+// (event_thread_barrier).  Rank streams stay process-lifetime objects all
+// the same — a CU-masked queue costs a KFD queue creation — : mpx_finalize
 // drains them (callback_fence), frees every allocation of the context, and
-// returns them to a per-device pool that later contexts reuse.  At exit they
-// are left to the runtime's teardown: every allocation their kernels touched
-// is freed by then — the safe order (profiles/r03_exit_order_ab.txt: 4 of 4
-// clean exits in processes mode, where destroying them in an exit handler
-// after callback_fence gave 2 of 4).  Round 3's exit-handler A/B modes
-// (MPX_POOL_EXIT) are gone.
+// returns them to a per-device pool that later contexts reuse; the host
+// destroys them with mpx_shutdown once no context is alive (mpx_perf in
+// both modes, bench.py).  A host that never calls it leaves them to the
+// runtime's exit teardown (every allocation their kernels touched is freed by
+// then: the safe order).
 struct StreamPool {
     std::mutex mu;
     std::map<int, std::vector<hipStream_t>> idle;    // per device
@@ -421,25 +493,70 @@ StreamPool& pool() {
 
 void fence_cb(void* p) { static_cast<std::atomic<int>*>(p)->fetch_add(1, std::memory_order_release); }
 
-// Before rank streams are destroyed.  hipStreamSynchronize returns when a
-// stream's commands are complete, but the runtime's HSA event thread may
-// still be inside the completion callback of the last one; a stream
-// destroyed under that callback leaves the thread waiting forever, and the
-// process stalls at exit (profiles/r02_exit_stall.txt) or in a later
-// context.  So two host functions go onto each stream as its last commands,
-// and the destroy waits until the SECOND has run: the event thread runs a
-// stream's callbacks in order, so by then every callback before it,
-// the first host function included, has returned.  The stream is drained
-// once more (its last command: the second host function) and then destroyed.
-// Minimal repro without libmpx (tools/exit_stall_repro.hip,
-// tools/gpu_exit_stall.sh; profiles/r03_exit_stall_repro.jsonl): two
-// CU-masked streams, 300 x {64 KiB copy, one-lane kernel} each, drained,
-// destroyed, exit — 8 of 10 processes stalled at exit with the destroy
-// right after the drain, 0 of 10 with this fence (0 of 10 with a 50 ms
-// sleep, round 2's workaround, now removed).  The wait for the callbacks is
-// bounded (10 s) only so that a runtime that never runs them cannot hang
-// the caller; the order, not the time, is what the fence relies on.
-void callback_fence(const std::vector<std::pair<int, hipStream_t>>& ss) {
+// Hands off twice through the HSA async-events thread, the one thread that
+// runs every hsa_amd_signal_async_handler callback, serially (hsa_ext_amd.h)
+// — HIP's command-completion handlers, which run host functions, among them.
+// When the second hand-off has run, every handler whose signal was satisfied
+// before the first was registered has returned (one pass of the events loop
+// fires every satisfied signal, in an arbitrary order: hence two).  One
+// signal serves the process (value 0, condition EQ 0: satisfied at once;
+// each registration returns false and is dropped).  Bounded at 10 s like the
+// fence; false if the thread never came round.
+bool on_events_thread(hsa_signal_value_t, void* arg) {
+    static_cast<std::atomic<int>*>(arg)->store(1, std::memory_order_release);
+    return false;
+}
+
+bool event_thread_barrier() {
+    static hsa_signal_t sig = [] {
+        hsa_signal_t s{0};
+        if (hsa_signal_create(0, 0, nullptr, &s) != HSA_STATUS_SUCCESS) s.handle = 0;
+        return s;
+    }();
+    if (!sig.handle) return false;
+    const double t_end = now_s() + 10.0;
+    for (int k = 0; k < 2; ++k) {
+        // heap-held: leaked if the bound expires, so a late handler never
+        // writes a dead stack frame
+        std::atomic<int>* done = new std::atomic<int>(0);
+        if (hsa_amd_signal_async_handler(sig, HSA_SIGNAL_CONDITION_EQ, 0, on_events_thread, done) != HSA_STATUS_SUCCESS) {
+            delete done;
+            return false;
+        }
+        while (!done->load(std::memory_order_acquire) && now_s() < t_end) usleep(20);
+        if (!done->load(std::memory_order_acquire)) return false;
+        delete done;
+    }
+    return true;
+}
+
+// Before streams are destroyed (and before the memory their commands used is
+// freed).  Why (round 5, symbolized from profiles/r04_procs_exit_stall.txt;
+// DESIGN.md §5 "Exit"): HIP's completion handler of a stream's command runs
+// on the HSA async-events thread and holds a reference to the stream's
+// virtual device until it returns — after the host function it ran.  When
+// hipStreamDestroy drops the stream's own reference first, the handler's
+// release is the last one: ~VirtualGPU runs ON the events thread, takes the
+// device's virtual-GPU lock, and for a CU-masked stream (never pooled)
+// hsa_queue_destroy's AqlQueue destructor waits, with no timeout, in the KFD
+// event wait (AMDKFD_IOC_WAIT_EVENTS) for the queue's inactive-signal
+// handler — which only that same thread can run.  The thread never returns;
+// the next runtime call that needs the lock (a later stream teardown, or the
+// fat-binary unregistration at exit) waits forever.  hipStreamSynchronize
+// and the host functions below cannot close that window: they return when the
+// command completed or the host function ran, both BEFORE the handler's
+// release.  So: two host functions go onto each stream as its last commands
+// (every callback before the second has returned once it runs), the streams
+// are drained, and then event_thread_barrier() waits until the events
+// thread has come round twice, i.e. has left the handler that ran the second
+// host function and dropped its reference.  After that the caller's
+// hipStreamDestroy drops the last reference on its own thread.
+// Repro without libmpx: tools/exit_stall_repro cycle_fence|cycle_barrier
+// (profiles/r05_stream_teardown_cycles.jsonl).  The waits are bounded (10 s)
+// only so that a runtime that never runs the callbacks cannot hang the
+// caller; the order, not the time, is what the fence relies on.  Returns
+// false when a bound expired (the caller then must not destroy the streams).
+bool callback_fence(const std::vector<std::pair<int, hipStream_t>>& ss) {
     // heap-held counters: leaked if the bound expires, so a late callback
     // never writes freed memory
     std::atomic<int>* cnt = new std::atomic<int>[ss.size() ? ss.size() : 1];
@@ -464,6 +581,9 @@ void callback_fence(const std::vector<std::pair<int, hipStream_t>>& ss) {
     if (prev >= 0) (void)hipSetDevice(prev);
     if (done) delete[] cnt;
     else if (getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] callback fence: host functions did not run in 10 s\n");
+    const bool handed_off = event_thread_barrier();
+    if (!handed_off && getenv("MPX_DEBUG")) fprintf(stderr, "[mpx] callback fence: events-thread barrier did not complete\n");
+    return done && handed_off;
 }
 
 // A rank stream goes back to the pool; it is never destroyed while the
@@ -1272,24 +1392,24 @@ int run_rccl(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
         const void* src = skip == i + 1 ? (const void*)me.rx : (const void*)me.tx;
         if (mode == MPX_MODE_PINGPONG) {
             if (group == 1) {
-                NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
-                NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Send(src, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Recv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, len, i, iters));
             } else {
-                NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Recv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, len, i, iters));
-                NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Send(src, n, ncclChar, peer_rank, me.comm, me.stream));
             }
             launches += 2;
         } else if (mode == MPX_MODE_UNIDIR) {
             if (group == 1) {
-                NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
-                NCCLCK(ncclRecv(me.rx, 1, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Send(src, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Recv(me.rx, 1, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, 1, i, iters));
             } else {
-                NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Recv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
                 if (check) TRY(stream_check(me, len, i, iters));
-                NCCLCK(ncclSend(src, 1, ncclChar, peer_rank, me.comm, me.stream));
+                NCCLCK(rccl_api().Send(src, 1, ncclChar, peer_rank, me.comm, me.stream));
             }
             launches += 2;
         } else {
@@ -1298,10 +1418,10 @@ int run_rccl(Rank& me, Rank& peer, int my_rank, int peer_rank, int mode, int gro
             // poisoned) on this stream before the next group's receive can
             // land — RCCL writes only this rank's own buffer, so no slots or
             // credits are needed; the device counts the Waitall receives.
-            NCCLCK(ncclGroupStart());
-            NCCLCK(ncclSend(src, n, ncclChar, peer_rank, me.comm, me.stream));
-            NCCLCK(ncclRecv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
-            NCCLCK(ncclGroupEnd());
+            NCCLCK(rccl_api().GroupStart());
+            NCCLCK(rccl_api().Send(src, n, ncclChar, peer_rank, me.comm, me.stream));
+            NCCLCK(rccl_api().Recv(me.rx, n, ncclChar, peer_rank, me.comm, me.stream));
+            NCCLCK(rccl_api().GroupEnd());
             launches += 1;
             if (check) {
                 TRY(stream_check(me, len, i, iters));
@@ -1427,12 +1547,12 @@ int mpx_finalize(mpx_ctx* ctx) {
             DeviceGuard g(rk.dev);
             (void)disarm(rk);
         }
-        if (rk.comm) (void)ncclCommDestroy(rk.comm);
+        if (rk.comm) (void)rccl_api().CommDestroy(rk.comm);
         rk.comm = nullptr;
         if (rk.local && rk.stream) ss.emplace_back(rk.dev, rk.stream);
     }
     for (auto& kv : ctx->dev_stream) ss.emplace_back(kv.first, kv.second);
-    callback_fence(ss);
+    const bool fenced = callback_fence(ss);
     DBG("finalize: streams drained\n");
     for (int i = 0; i < MPX_MAX_RANKS; ++i) {
         for (auto& kv : ctx->r[i].sdma_graphs) (void)hipGraphExecDestroy(kv.second);
@@ -1471,9 +1591,11 @@ int mpx_finalize(mpx_ctx* ctx) {
         if (rk.ev1) (void)hipEventDestroy(rk.ev1);
         if (rk.stream) release_rank_stream(rk.dev, rk.stream);
     }
-    for (auto& kv : ctx->dev_stream) {
-        DeviceGuard g(kv.first);
-        (void)hipStreamDestroy(kv.second);
+    if (fenced) {   // else left to the runtime: a destroy could be the events thread's last release
+        for (auto& kv : ctx->dev_stream) {
+            DeviceGuard g(kv.first);
+            (void)hipStreamDestroy(kv.second);
+        }
     }
     DBG("finalize: done\n");
     delete ctx;
@@ -2000,10 +2122,10 @@ int rccl_link(Rank& me, int my_rank, int peer_rank) {
     if (me.rccl_linked[peer_rank]) return MPX_OK;
     DeviceGuard g(me.dev);
     HIPCK(g.err);
-    NCCLCK(ncclGroupStart());
-    NCCLCK(ncclSend(me.scratch + kScrLink, 1, ncclChar, peer_rank, me.comm, me.stream));
-    NCCLCK(ncclRecv(me.scratch + kScrLink + 1, 1, ncclChar, peer_rank, me.comm, me.stream));
-    NCCLCK(ncclGroupEnd());
+    NCCLCK(rccl_api().GroupStart());
+    NCCLCK(rccl_api().Send(me.scratch + kScrLink, 1, ncclChar, peer_rank, me.comm, me.stream));
+    NCCLCK(rccl_api().Recv(me.scratch + kScrLink + 1, 1, ncclChar, peer_rank, me.comm, me.stream));
+    NCCLCK(rccl_api().GroupEnd());
     HIPCK(hipStreamSynchronize(me.stream));
     me.rccl_linked[peer_rank] = true;
     return MPX_OK;
@@ -2053,7 +2175,8 @@ int mpx_shutdown(void) {
     std::lock_guard<std::mutex> lk(p.mu);
     if (p.live_contexts != 0) return fail(MPX_ERR_STATE, "%d contexts are still alive", p.live_contexts);
     if (p.all.empty()) return MPX_OK;
-    callback_fence(p.all);
+    if (!callback_fence(p.all))
+        return fail(MPX_ERR_TIMEOUT, "stream fence did not complete in 10 s: streams left to the runtime");
     int prev = -1;
     (void)hipGetDevice(&prev);
     for (auto& ds : p.all) {
@@ -2089,19 +2212,18 @@ int mpx_barrier(mpx_ctx* ctx, int nthreads) {
 
 int mpx_rccl_version(int* version, char* path, int len) {
     if (!version || !path || len < 64) return fail(MPX_ERR_INVALID, "bad argument");
-    NCCLCK(ncclGetVersion(version));
-    Dl_info info{};
-    const char* where = dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) && info.dli_fname ? info.dli_fname
-                                                                                                 : "(unknown)";
-    snprintf(path, (size_t)len, "%s", where);
+    RCCL_LOADED();
+    NCCLCK(rccl_api().GetVersion(version));
+    snprintf(path, (size_t)len, "%s", rccl_api().path);
     return MPX_OK;
 }
 
 int mpx_rccl_get_unique_id(void* id) {
     if (!id) return fail(MPX_ERR_INVALID, "id is NULL");
     static_assert(sizeof(ncclUniqueId) == MPX_RCCL_ID_BYTES, "RCCL unique id size");
+    RCCL_LOADED();
     ncclUniqueId u;
-    NCCLCK(ncclGetUniqueId(&u));
+    NCCLCK(rccl_api().GetUniqueId(&u));
     memcpy(id, &u, sizeof u);
     return MPX_OK;
 }
@@ -2111,11 +2233,12 @@ int mpx_rccl_init_rank(mpx_ctx* ctx, int rank, int nranks, const void* id) {
     if (rank < 0 || rank >= ctx->nranks || !ctx->r[rank].local) return fail(MPX_ERR_STATE, "rank %d is not attached", rank);
     Rank& rk = ctx->r[rank];
     if (rk.comm) return fail(MPX_ERR_STATE, "rank %d already has a communicator", rank);
+    RCCL_LOADED();
     DeviceGuard g(rk.dev);
     HIPCK(g.err);
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
-    NCCLCK(ncclCommInitRank(&rk.comm, nranks, u, rank));
+    NCCLCK(rccl_api().CommInitRank(&rk.comm, nranks, u, rank));
     rk.comm_rank = rank;
     return MPX_OK;
 }
@@ -2128,8 +2251,9 @@ int mpx_rccl_init_all(mpx_ctx* ctx) {
         if (ctx->r[i].comm) return fail(MPX_ERR_STATE, "rank %d already has a communicator", i);
         devs.push_back(ctx->r[i].dev);
     }
+    RCCL_LOADED();
     std::vector<ncclComm_t> comms(devs.size());
-    NCCLCK(ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()));
+    NCCLCK(rccl_api().CommInitAll(comms.data(), (int)devs.size(), devs.data()));
     for (int i = 0; i < ctx->nranks; ++i) {
         ctx->r[i].comm = comms[i];
         ctx->r[i].comm_rank = i;

@@ -744,10 +744,14 @@ int main(int argc, char **argv)
         rank_main((void *)(intptr_t)me);
         barrier(); /* MPI_Barrier, mpi_perf.c:579: no peer still maps our buffers */
         if (ctx) MPX_CHECK(mpx_finalize(ctx)); /* frees tx/rx too */
-        /* the pooled rank streams are left to the runtime's exit teardown:
-           destroying them here (mpx_shutdown) stalled 1 exit in 4 in this
-           mode (profiles/r04_procs_exit_stall.txt), as round 3's exit-handler
-           destroy did */
+        /* the pooled rank streams go before exit, as in threads mode below.
+           Round 4 left them to the runtime here: the destroy stalled 1 exit
+           in 4 (profiles/r04_procs_exit_stall.txt) — HIP's completion handler
+           of the stream's last host function dropped the last reference on
+           the HSA events thread, whose queue destroy then waited for itself.
+           mpx_shutdown's fence now waits for that handler to return first
+           (event_thread_barrier, DESIGN.md §5 "Exit"). */
+        if (ctx) MPX_CHECK(mpx_shutdown());
         barrier();
         mpxb_spin_close(start_bar, 0);
         mpxb_finalize(boot);

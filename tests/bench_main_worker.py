@@ -29,6 +29,6 @@ torch.cuda.synchronize = lambda *a: None
 bench.EXTRAS_DEADLINE_S = 5
 sys.argv = ["bench.py"] + sys.argv[2:]
 bench.main()
-# reached only when main() returns instead of ending the process itself
-# (os._exit): the profiled exit, which must have destroyed the rank streams
+# main() returns through the normal exit after destroying the rank streams
+# (mpx_shutdown), profiled or not (round 5: no os._exit after the line)
 print(f"MAIN_RETURNED shutdown={any(x[0] == 'shutdown' for x in W.FakeMpx.log)}", file=sys.stderr, flush=True)

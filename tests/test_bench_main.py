@@ -70,18 +70,16 @@ def test_one_json_line_with_the_contract_keys():
 
 
 def test_exit_path_with_and_without_a_profiler():
-    """Unprofiled, every rank ends itself after its line (os._exit: no
-    exit-time runtime teardown).  Under rocprofv3 (one of its variables set;
-    ROCPROF_COUNTERS here — the tool-library variable would make the SDK in
-    this process try to load that library) every rank destroys its rank
-    streams (mpx_shutdown) and returns through the normal exit, where the
-    profiler writes its output; the in-process counters stand aside (one
-    rocprofiler tool per process)."""
-    rcs, outs = run("ok")
-    assert rcs == [0, 0] and not any("MAIN_RETURNED" in o[1] for o in outs)
-    rcs, outs = run("ok", extra_env={"ROCPROF_COUNTERS": "FETCH_SIZE"})
-    assert rcs == [0, 0], [o[1][-600:] for o in outs]
-    assert all("MAIN_RETURNED shutdown=True" in o[1] for o in outs), [o[1][-300:] for o in outs]
+    """Every rank destroys its rank streams (mpx_shutdown) after its line and
+    returns through the normal exit, profiled or not (round 5: the
+    os._exit(0) of round 4 is gone, DESIGN.md §5 "Exit").  Under rocprofv3
+    (one of its variables set; ROCPROF_COUNTERS here — the tool-library
+    variable would make the SDK in this process try to load that library)
+    the in-process counters stand aside (one rocprofiler tool per process)."""
+    for env in (None, {"ROCPROF_COUNTERS": "FETCH_SIZE"}):
+        rcs, outs = run("ok", extra_env=env)
+        assert rcs == [0, 0], [o[1][-600:] for o in outs]
+        assert all("MAIN_RETURNED shutdown=True" in o[1] for o in outs), [o[1][-300:] for o in outs]
     d = lines(outs[0][0])[0]
     assert d["roofline"]["traffic"] is None and "under a profiler" in d["roofline"]["traffic_source"]
 
