@@ -361,6 +361,14 @@ def safe_wall(c, errs: list, *xfer_args, barrier=None, **xfer_kw) -> float:
         return c.xfer(*xfer_args, timeout_ms=POST_TIMEOUT_MS, **xfer_kw).wall_s
     except Exception as e:  # noqa: BLE001
         errs.append(f"{type(e).__name__}: {e}"[:240])
+        # a call armed for this transfer whose start never came (the barrier
+        # in front of it failed) is cancelled here: left armed, every later
+        # arm and transfer of this rank would be refused and its kernel would
+        # spin until its go deadline.  A no-op when not armed.
+        try:
+            c.disarm(xfer_args[2])
+        except Exception as e2:  # noqa: BLE001
+            errs.append(f"disarm: {type(e2).__name__}: {e2}"[:240])
         return float("inf")
 
 
@@ -908,6 +916,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     out["push"] = push_name(nwg, stream) if nwg else "default"
 
     step_err = []
+    timed_armed = []   # per timed G1 step: started from an armed launch (kernel-span clock)
 
     def step(s: int):
         g, peer = round_role(rounds, s % len(rounds), rank)
@@ -923,8 +932,10 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
         try:
             # MPI_Barrier (mpi_perf.c:499), then the loop: one C call with
             # the spin barrier (start_after_barrier)
-            return g, start_after_barrier(dist, c, mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg,
-                                          stream=stream, **pkw)
+            t = start_after_barrier(dist, c, mpx.MODE_UNIDIR, g, rank, peer, iters, tx, rx, nbytes, nwg=nwg,
+                                    stream=stream, **pkw)
+            step.armed = armed and engine == "kernel"
+            return g, t
         except Exception as e:  # noqa: BLE001
             step_err.append(f"rank {rank}: step {s}: {type(e).__name__}: {e}"[:300])
             return g, None
@@ -953,6 +964,7 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
             n_sends += 1
             step_dev[s] = t.device_s
             step_nwg = t.nwg
+            timed_armed.append(step.armed)
     barrier_sync()
     elapsed = time.perf_counter() - t0
     err = agree(step_err[0] if step_err else "")
@@ -968,6 +980,16 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
     dist.all_reduce(st, op=dist.ReduceOp.SUM)
     out["per_launch_s"] = float(st[0]) / max(float(st[1]), 1.0)
     out["per_pair_GBps"] = nbytes * iters / out["per_launch_s"] / 1e9
+    # which clock per_launch_s is on: an armed kernel-engine
+    # call's device time is the kernel's own span, from the moment workgroup 0
+    # sees the go word to the last workgroup's end (s_memrealtime); an
+    # unarmed call's (and the stream engines') is the HIP-event span, launch
+    # included.  Rounds 1-3 were all "events".
+    na = torch.tensor([float(sum(timed_armed)), float(len(timed_armed))], dtype=torch.float64)
+    dist.all_reduce(na, op=dist.ReduceOp.SUM)
+    out["device_clock"] = ("kernel-span (armed: go seen -> last workgroup end, s_memrealtime)" if na[0] == na[1] and na[1]
+                           else "events (HIP events around the launch)" if na[0] == 0
+                           else f"mixed: {int(na[0])} of {int(na[1])} G1 launches armed (kernel span), the rest events")
     out.update(pair_table(torch, dist, rounds, rank, world, steps, step_dev, step_wall, nbytes * iters))
     nw = torch.tensor([float(step_nwg)], dtype=torch.float64)
     dist.all_reduce(nw, op=dist.ReduceOp.MAX)
@@ -1311,7 +1333,8 @@ def main() -> None:
                     peak_note="one direction of one xGMI link (153.6 GB/s bidirectional per link)",
                     frac_of_bidirectional_link=round(achieved / XGMI_LINK_PEAK_BIDIR_GBPS, 4),
                     kernel="k_xfer (G1 side)" if engine_used == "kernel" else engine_used,
-                    avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters)
+                    avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters,
+                    device_clock=res.get("device_clock"))
         if os.environ.get("MPX_BENCH_ONE_GPU"):
             roof["rehearsal_note"] = ("one-GPU rehearsal: every rank on one card, so achieved is a loopback (HBM) "
                                       "rate and frac against the link peak says nothing about a link")
@@ -1492,6 +1515,9 @@ def main() -> None:
     # finalizer while rank streams were alive (profiles/r04_exit_segv_stack.txt),
     # and the destroy had stalled 1 processes-mode exit in 4 — root-caused in
     # round 5 (DESIGN.md §5 "Exit") and closed by mpx_shutdown's fence.
+    # the marker tools/node_profile.sh tells an exit-time stall by (a rank
+    # that printed it and then ran out of time finished its transfers)
+    print(f"[bench] rank {rank}: done, shutting down", file=sys.stderr)
     sys.stdout.flush()
     sys.stderr.flush()
     mpx.shutdown()

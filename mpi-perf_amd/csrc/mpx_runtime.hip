@@ -418,6 +418,9 @@ u64 nb_waited(int iters) {
 //                   negative control of tests/test_gpu_ordering.py
 //   no_pull_wait    pull mode: a sending side returns without waiting for the
 //                   peer's loads of its tx (the buffer-reuse negative control)
+//   fail_launch=r   rank r's kernel-engine calls fail before their kernel is
+//                   enqueued (after prepare_call took their numbers): the
+//                   rollback test of unprepare_call
 // Whether the variable exists is read ONCE per process: a process that
 // starts without it (bench.py, mpx_perf) never looks again, and none of the
 // knobs can reach it.  The tests set it (empty) before their first call
@@ -427,6 +430,7 @@ struct TestKnobs {
     int lag_rank = -1, lag_wg = 0;
     long long lag_us = 0;
     bool no_posted = false, no_pull_wait = false;
+    int fail_launch = -1;
 };
 TestKnobs test_knobs() {
     static const bool gate = getenv("MPX_TEST") != nullptr;
@@ -445,6 +449,7 @@ TestKnobs test_knobs() {
             if (sscanf(item.c_str() + 7, "%d:%d:%lld", &k.lag_rank, &k.lag_wg, &k.lag_us) != 3) k.lag_rank = -1;
         } else if (item == "no_posted") k.no_posted = true;
         else if (item == "no_pull_wait") k.no_pull_wait = true;
+        else if (!item.compare(0, 12, "fail_launch=")) k.fail_launch = atoi(item.c_str() + 12);
         pos = end + 1;
     }
     return k;
@@ -716,7 +721,20 @@ struct KernelCall {
     uint64_t expect = 0, expect_ack = 0;
     double t_launch = 0;
     bool resident = false;   // armed: every workgroup was waiting when arm returned
+    bool took_call = false;  // prepare_call took a call number on the link (iters > 0)
+    bool launched = false;   // the kernel was enqueued: the call number is spent
 };
+
+// A call that failed before its kernel was enqueued gives back what
+// prepare_call took (its token and the link's call number): the peer never
+// sees that number, and a later call must post the one the peer waits for
+// (ADVICE r04).  Once the kernel is enqueued the numbers stay taken — the
+// kernel posts them — whatever fails after it.
+void unprepare_call(Rank& me, const KernelCall& kc) {
+    if (kc.launched) return;
+    if (kc.took_call) --me.calls[kc.peer_rank];
+    --me.token;
+}
 
 // Wait for the call's completion.  Unarmed: the end event ev1 (see
 // sync_mode); *t_done = when the completion word was first seen (0 in event
@@ -867,7 +885,8 @@ int prepare_call(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank,
     a.done_token = ++me.token;
     // a call that moves nothing (iters = 0) posts nothing new: the count
     // stays equal on both sides even if only one side makes such a call
-    a.call = iters > 0 ? ++me.calls[peer_rank] : me.calls[peer_rank];
+    kc->took_call = iters > 0;
+    a.call = kc->took_call ? ++me.calls[peer_rank] : me.calls[peer_rank];
     if (knobs.no_posted) a.call = 0;   // every wait for posted >= 0 holds at once
     kc->ll = ll;
     kc->my_rank = my_rank;
@@ -891,6 +910,8 @@ int prepare_call(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank,
 // comes from its own clock).
 int launch_call(Rank& me, KernelCall& kc, bool armed) {
     XferArgs& a = kc.a;
+    if (test_knobs().fail_launch == kc.my_rank)
+        return fail(MPX_ERR_HIP, "rank %d: launch failed (MPX_TEST fail_launch)", kc.my_rank);
     if (a.check) {
         HIPCK(hipMemsetAsync(me.csum, 0, (size_t)kc.iters * sizeof(u64), me.stream));
         if (kc.mode == MPX_MODE_NONBLOCKING)
@@ -906,11 +927,13 @@ int launch_call(Rank& me, KernelCall& kc, bool armed) {
         a.go_timeout_ticks = std::max<u64>(a.timeout_ticks, 60ull * 100000000ull);
         kc.t_launch = now_s();
         HIPCK(launch_xfer(a, kc.grid, me.stream));
+        kc.launched = true;
         return MPX_OK;
     }
     kc.t_launch = now_s();
     HIPCK(hipEventRecord(me.ev0, me.stream));
     HIPCK(launch_xfer(a, kc.grid, me.stream));
+    kc.launched = true;
     HIPCK(hipEventRecord(me.ev1, me.stream));
     return MPX_OK;
 }
@@ -983,7 +1006,11 @@ int run_kernel(mpx_ctx* ctx, Rank& me, Rank& peer, int my_rank, int peer_rank, i
     const double t_call = now_s();
     KernelCall kc;
     TRY(prepare_call(ctx, me, peer, my_rank, peer_rank, mode, group, iters, len, o, &kc));
-    TRY(launch_call(me, kc, false));
+    const int st = launch_call(me, kc, false);
+    if (st != MPX_OK) {
+        unprepare_call(me, kc);
+        return st;
+    }
     return complete_call(me, kc, false, t_call, kc.t_launch, t);
 }
 
@@ -996,7 +1023,7 @@ int disarm(Rank& me) {
     __atomic_store_n(&me.status->go, kc.a.go_token | kGoCancel, __ATOMIC_RELEASE);
     double t_done = 0;
     const int st = wait_kernel(me, kc.a.done_token, true, &t_done);
-    if (kc.iters > 0 && !test_knobs().no_posted) --me.calls[kc.peer_rank];
+    if (kc.took_call) --me.calls[kc.peer_rank];   // the same condition prepare_call took it on
     delete me.armed;
     me.armed = nullptr;
     return st;
@@ -2040,9 +2067,24 @@ int mpx_xfer_arm(mpx_ctx* ctx, int mode, int my_group, int my_rank, int peer_ran
     HIPCK(g.err);
     KernelCall* kc = new KernelCall;
     int st = prepare_call(ctx, me, peer, my_rank, peer_rank, mode, my_group, iters, buff_len, opts, kc);
-    if (st == MPX_OK) st = launch_call(me, *kc, true);
     if (st != MPX_OK) {
         delete kc;
+        return st;
+    }
+    st = launch_call(me, *kc, true);
+    if (st != MPX_OK) {
+        // not launched: give the numbers back, and the inline call the
+        // caller falls back to posts the one the peer waits for.  Launched
+        // (a failure after the enqueue): the kernel waits for a go it will
+        // never get — cancel it as disarm does, which also returns the call
+        // number (the kernel exits before posting its receives)
+        if (kc->launched) {
+            me.armed = kc;
+            (void)disarm(me);
+        } else {
+            unprepare_call(me, *kc);
+            delete kc;
+        }
         return st;
     }
     // Until the whole grid runs (Status.ready), a start would also wait for

@@ -67,6 +67,7 @@ def test_one_json_line_with_the_contract_keys():
     assert d["extras"]["unidir_4MiB_unstaged_GBps"] is not None
     assert d["extras"]["hbv3_rounds_unidir"]["phases_us_median"]["g1"]["kernel_s"] == 1.0
     assert d["config"]["barrier"].startswith("node-local spin barrier") and d["config"]["launch"].startswith("armed")
+    assert d["roofline"]["device_clock"].startswith("kernel-span (armed")
 
 
 def test_exit_path_with_and_without_a_profiler():

@@ -108,6 +108,32 @@ def test_disarmed_calls_leave_the_link_in_step(mode):
         P.close()
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_failed_launch_gives_its_call_number_back(mode, monkeypatch):
+    """A call whose launch fails after prepare_call took its numbers
+    (MPX_TEST fail_launch=0: rank 0's kernel is never enqueued), armed and
+    unarmed, then normal calls on the same link: they must pass every check.
+    Without the rollback, rank 0 posts a call number one higher than rank 1
+    ever sends and every later call times out."""
+    P = Pairs("kernel", 1, 1 << 20, fill="seeded")
+    try:
+        c = P.c
+        monkeypatch.setenv("MPX_TEST", "fail_launch=0")
+        with pytest.raises(mpx.MpxError) as e:
+            c.arm(mode, P.group(0), 0, 1, 9, P.bufs[0][0], P.bufs[0][1], 70000)
+        assert "fail_launch" in str(e.value)
+        with pytest.raises(mpx.MpxError) as e:
+            c.xfer(mode, P.group(0), 0, 1, 9, P.bufs[0][0], P.bufs[0][1], 70000)
+        assert "fail_launch" in str(e.value)
+        monkeypatch.setenv("MPX_TEST", "")
+        for armed in (False, True, False):
+            out, errs = P.run(mode, 70000, 9, armed=armed)
+            assert not errs, (armed, errs)
+            assert all(out[r].check_failures == 0 and out[r].check_iters == 9 for r in (0, 1))
+    finally:
+        P.close()
+
+
 def test_finalize_cancels_an_armed_call():
     """mpx_finalize with armed ranks: the kernels are cancelled and the
     context closes; a new context on the same GPU then works."""

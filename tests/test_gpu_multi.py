@@ -17,7 +17,7 @@ compared with the compiled reference's golden runs where one exists.
 MPX_MULTI_REHEARSE=1 (with MPX_LL_MAX=8192, the cross-GPU LL threshold) runs
 this module on ONE GPU, every rank on GPU 0 and N = MPX_MULTI_REHEARSE_N
 (default 4) ranks where a test uses the whole node: it proves the tests'
-own code, not the links (tools/gpu_multi_rehearse.sh).  What only distinct
+own code, not the links (tools/gpu.sh multi_rehearse).  What only distinct
 GPUs have is skipped then: RCCL (it refuses two ranks on one GPU), the
 link table, and the "every pair spans two GPUs" check.
 """

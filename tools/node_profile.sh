@@ -47,8 +47,20 @@ run_pass() {   # pass-name, rocprofv3 options...
         fi
         pids+=($!)
     done
-    local rc=0 p
-    for p in "${pids[@]}"; do wait $p || rc=1; done
+    # a rank that timed out after bench.py's "done, shutting down" marker
+    # finished its transfers and stalled at exit: reported on its own, so an
+    # exit stall is never read as a transfer failure
+    local rc=0 i x
+    for i in "${!pids[@]}"; do
+        wait ${pids[$i]}; x=$?
+        [ $x -eq 0 ] && continue
+        rc=1
+        if { [ $x -eq 124 ] || [ $x -eq 137 ]; } && grep -q "done, shutting down" $O/${pass}_rank$i.err; then
+            echo "node_profile N=$N pass $pass rank $i: EXIT STALL (rc $x after its transfers finished)"
+        else
+            echo "node_profile N=$N pass $pass rank $i: FAILED rc $x"
+        fi
+    done
     echo "node_profile N=$N pass $pass rc=$rc"
     return $rc
 }

@@ -1,10 +1,13 @@
-"""Summarise tools/gpu_pmc_xfer.sh's passes into profiles/r02_pmc_xfer.json:
+"""Summarise tools/gpu.sh pmc_xfer's passes into profiles/r02_pmc_xfer.json:
 HBM bytes per push (per iteration for the pair cases) of the pair kernel,
 against its B.  FETCH_SIZE is doubled and WRITE_SIZE taken as is
 (MI355X_MICROARCH.md §HBM, gfx950); both are the L2's memory-side request
 counters, device-wide, so a pair case counts both halves' traffic.
 
-    python tools/pmc_xfer_summary.py gpurun_out/pmc_xfer profiles/r02_pmc_xfer.json
+    python tools/pmc_xfer_summary.py gpurun_out/<tag> profiles/<round>_pmc_xfer.json
+
+(cases are the pmc_<name>_{FETCH,WRITE}_SIZE pass directories with their
+.log; other passes in the same directory, e.g. the bench's, are skipped)
 """
 import csv
 import glob
@@ -36,7 +39,7 @@ res = []
 for name in cases:
     f = glob.glob(os.path.join(src, f"{name}_FETCH_SIZE", "*counter_collection.csv"))
     w = glob.glob(os.path.join(src, f"{name}_WRITE_SIZE", "*counter_collection.csv"))
-    if not f or not w:
+    if not f or not w or not os.path.exists(os.path.join(src, f"{name}_WRITE_SIZE.log")):
         continue
     fkb, nf, kname = kb(f[0], "FETCH_SIZE")
     wkb, nw, _ = kb(w[0], "WRITE_SIZE")
@@ -51,7 +54,7 @@ for name in cases:
                     hbm_read_bytes_per_iter=round(read_pp, 1), hbm_write_bytes_per_iter=round(write_pp, 1),
                     read_over_B=round(read_pp / B, 3) if B else None, write_over_B=round(write_pp / B, 3) if B else None,
                     us_per_iter=wl.get("us_per_push", wl.get("us_per_iter"))))
-doc = dict(source="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/gpu_pmc_xfer.sh); "
+doc = dict(source="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/gpu.sh pmc_xfer); "
                   "FETCH_SIZE x2 per MI355X_MICROARCH.md HBM section; median of 3 dispatches of 'iters' iterations",
            cases=res)
 json.dump(doc, open(out, "w"), indent=1)

@@ -1,7 +1,7 @@
 """A rank paired with itself on the SDMA engine (the non-blocking loop as
 MPI's self-send): its payload copies are hipMemcpyDeviceToDeviceNoCU, i.e.
 copy-engine (SDMA) transfers even on one GPU — profiled by
-tools/gpu_prof_sdma.sh with --memory-copy-trace.  Every payload of the first
+tools/gpu.sh prof_sdma with --memory-copy-trace.  Every payload of the first
 call is checked; prints one JSON line."""
 import json
 import os
