@@ -113,6 +113,51 @@ def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:
     return None
 
 
+def cpu_baseline_pingpong(runs: int = 6) -> dict | None:
+    """BASELINE config 1 on the box's own host cores:
+    the compiled reference's 2-rank ping-pong (mpi_perf.c:66-83, the default
+    loop) under MPICH shm at 8 B (-i 20000) and 4 MiB (-i 500), SURVEY
+    §8(d) cfg1's iterations, -r runs; median of runs 1..runs-1 (run 0 is the
+    reference's warm-up).  half_rtt_us_8B = time / (2 x iters); GBps_4MiB =
+    2 x B x iters / time, the reference's own formula for this loop
+    (mpi_perf.c:535-542, both directions).  ~5 s on the box, before any GPU
+    call."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not (os.path.exists(ref) and os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libshim.so"))
+            and os.path.exists(mpiexec)):
+        return None
+    out = dict(cores=2, kind="reference", loop="ping-pong (mpi_perf.c:66-83)",
+               sample=f"mpi_perf.c (oracle/_ref) under MPICH 3.3.2 shm, 2 ranks, -b 8 -i 20000 and -b 4194304 "
+                      f"-i 500, -r {runs}, median of runs 1..{runs - 1}")
+    for nbytes, iters, key in ((8, 20000, "half_rtt_us_8B"), (4 << 20, 500, "GBps_4MiB")):
+        tmp = tempfile.mkdtemp(prefix="cpu_base_pp_")
+        try:
+            with open(os.path.join(tmp, "group1"), "w") as f:
+                f.write("localhost\n")
+            os.mkdir(os.path.join(tmp, "logs"))
+            env = dict(os.environ)
+            env.pop("SHIM_OUT", None)
+            cmd = [mpiexec, "-np", "2", "-genv", "PPN", "1", "-genv", "HOST1", "localhost", "-genv", "HOST0",
+                   "127.0.0.1", os.path.join(ROOT, "oracle", "ref_wrap.sh"), ref, "-f", "group1", "-n", "1",
+                   "-p", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs), "-l", "logs"]
+            p = subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=120)
+            times = [float(line.split(",")[9]) / 1000.0 for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log"))
+                     for line in open(path)]
+            if p.returncode != 0 or not times:
+                out[key] = None
+                out[key + "_error"] = f"rc {p.returncode}: {p.stderr[-200:]}"
+                continue
+            t = statistics.median(times)
+            out[key] = round(t / (2 * iters) * 1e6, 3) if nbytes == 8 else round(2 * nbytes * iters / t / 1e9, 3)
+        except Exception as e:  # noqa: BLE001
+            out[key] = None
+            out[key + "_error"] = f"{type(e).__name__}: {e}"[:200]
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+    return out
+
+
 def cpu_baseline_pairs(world: int, nbytes: int, iters: int, runs: int) -> dict | None:
     """The reference itself on the host beside the N >= 2 line: run-hbv3's
     layout (scripts/run-hbv3.sh:22,28: N ranks, ppn = N/2 flows, -u 1) at the
@@ -717,6 +762,16 @@ def staged_vs_unstaged(mpx, torch, dist, c, rounds, rank, tx, rx, nbytes, iters,
 # (a bulk push of B bytes makes B / 64 64-B requests: profiles/r02_pmc_xfer_ea.json).
 LINK_COUNTERS = ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum", "TCC_EA0_WRREQ_DRAM_sum")
 READ_COUNTERS = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum")
+# where the non-DRAM writes go, in 32-B units (gfx950: "1 64-byte request
+# will be counted to 2"): the GMI (inter-die / xGMI) and IO (PCIe) paths
+FABRIC_COUNTERS = ("TCC_EA0_WRREQ_WRITE_GMI_32B_sum", "TCC_EA0_WRREQ_WRITE_IO_32B_sum",
+                   "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum")
+# the link bytes' self-check: on distinct GPUs the
+# subtraction must read the pushed bytes within this band, else the line
+# carries no traffic figure (null, with the raw counters and the reason)
+LINK_CHECK_BAND = (0.9, 1.1)
+COUNTER_SETS = (LINK_COUNTERS, READ_COUNTERS, FABRIC_COUNTERS)
+ALL_COUNTERS = LINK_COUNTERS + READ_COUNTERS + FABRIC_COUNTERS
 
 
 def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes, iters, nwg, stream, buses,
@@ -732,7 +787,7 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
     vals = {}
     g1_s, g1_n = 0.0, 0
     notes = []
-    for names in (LINK_COUNTERS, READ_COUNTERS):
+    for names in COUNTER_SETS:
         p = None
         if sampler:
             try:
@@ -756,8 +811,8 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
                 vals["reads_reset"] = p.reads_reset
             except Exception as e:  # noqa: BLE001
                 notes.append(f"rank {rank}: {type(e).__name__}: {e}"[:200])
-    mine = [1.0 if (sampler and all(k in vals for k in LINK_COUNTERS + READ_COUNTERS)) else 0.0]
-    mine += [float(vals.get(k, 0.0)) for k in LINK_COUNTERS + READ_COUNTERS] + [g1_s, float(g1_n)]
+    mine = [1.0 if (sampler and all(k in vals for k in ALL_COUNTERS)) else 0.0]
+    mine += [float(vals.get(k, 0.0)) for k in ALL_COUNTERS] + [g1_s, float(g1_n)]
     every = [torch.zeros(len(mine), dtype=torch.float64) for _ in range(world)]
     dist.all_gather(every, torch.tensor(mine, dtype=torch.float64))
     all_notes = [None] * world
@@ -767,23 +822,27 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
     got = [e for e in every if float(e[0]) == 1.0]
     if len(got) != want:
         return {"error": "; ".join(notes) or "not every GPU was sampled", "samplers": want, "sampled": len(got)}
-    tot = [sum(float(e[1 + k]) for e in got) for k in range(len(LINK_COUNTERS) + len(READ_COUNTERS))]
-    wr, w64, dram, rd, rd_dram = tot
+    tot = [sum(float(e[1 + k]) for e in got) for k in range(len(ALL_COUNTERS))]
+    wr, w64, dram, rd, rd_dram, gmi32, io32, dram32 = tot
     launches = (world // 2) * len(rounds)
     alg = nbytes * iters * launches
+    distinct = len(set(buses)) == world
     g1_avg = sum(float(e[-2]) for e in every) / max(sum(float(e[-1]) for e in every), 1.0)
     link = (wr - dram) * 64
     out = dict(
         source="in-process rocprofiler-sdk device counting service (mpi-perf_amd/lib/libmpxprof.so), one pass per "
                "counter set over an untimed re-run of every round (the timed steps' loop, width and hint), one "
                "sampling rank per GPU",
-        counters=list(LINK_COUNTERS + READ_COUNTERS), samplers=want, g1_launches_per_pass=launches,
+        counters=list(ALL_COUNTERS), samplers=want, g1_launches_per_pass=launches,
+        raw=dict(zip(ALL_COUNTERS, tot)), ranks_on_distinct_gpus=distinct,
         algorithmic_bytes_per_launch=nbytes * iters,
         link_bytes_per_launch=round(link / launches, 1),
         local_dram_write_bytes_per_launch=round(dram * 64 / launches, 1),
         link_over_algorithmic=round(link / alg, 5), local_dram_over_algorithmic=round(dram * 64 / alg, 5),
         write_requests_64B_fraction=round(w64 / wr, 5) if wr else None,
         read_requests_per_launch=round(rd / launches, 1), read_dram_requests_per_launch=round(rd_dram / launches, 1),
+        gmi_write_bytes_per_launch=round(gmi32 * 32 / launches, 1), io_write_bytes_per_launch=round(io32 * 32 / launches, 1),
+        gmi_over_algorithmic=round(gmi32 * 32 / alg, 5), io_over_algorithmic=round(io32 * 32 / alg, 5),
         g1_avg_launch_us=round(g1_avg * 1e6, 2),
         achieved_link_GBps_per_pair=round(link / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
         achieved_local_dram_GBps_per_pair=round(dram * 64 / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
@@ -791,6 +850,58 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
     if notes:
         out["notes"] = notes
     return out
+
+
+def link_traffic(cnt: dict) -> dict:
+    """roofline fields from link_counters' result, with the self-check
+    (VERDICT r04, next 2).  On distinct GPUs every pushed byte crosses a
+    link, so (WRREQ - WRREQ_DRAM) x 64 must read the pushed bytes: outside
+    LINK_CHECK_BAND the line prints NO traffic figure (null), with the raw
+    counters and the reason — a counter that cannot see the path's link
+    writes (e.g. if peer-HBM writes were classified as DRAM at the sender)
+    must not pass for a measurement of ~0.  When the ranks share a GPU
+    (the one-GPU rehearsal) the pushes are local and ~0 is the right
+    reading: no check applies."""
+    lo, hi = LINK_CHECK_BAND
+    r = cnt["link_over_algorithmic"]
+    src = ("xGMI link bytes per G1 launch: (TCC_EA0_WRREQ - TCC_EA0_WRREQ_DRAM) x 64 B of every GPU, summed; "
+           + cnt["source"])
+    if not cnt.get("ranks_on_distinct_gpus"):
+        return dict(traffic=cnt["link_bytes_per_launch"], traffic_local_dram=cnt["local_dram_write_bytes_per_launch"],
+                    traffic_source=src, traffic_check="not applicable: ranks share a GPU (local pushes, ~0 expected)")
+    if lo <= r <= hi:
+        return dict(traffic=cnt["link_bytes_per_launch"], traffic_local_dram=cnt["local_dram_write_bytes_per_launch"],
+                    traffic_source=src, traffic_check=f"passed: link bytes {r} x the pushed bytes (band {lo}-{hi})")
+    return dict(traffic=None, traffic_local_dram=cnt["local_dram_write_bytes_per_launch"], traffic_source=src,
+                traffic_check="failed",
+                traffic_reason=(f"link-byte self-check failed: (WRREQ - WRREQ_DRAM) x 64 read {r} x the pushed bytes "
+                                f"(band {lo}-{hi}); the GMI 32-B write counter reads {cnt.get('gmi_over_algorithmic')}, "
+                                f"IO {cnt.get('io_over_algorithmic')}, local DRAM "
+                                f"{cnt.get('local_dram_over_algorithmic')} x: the counters do not see this path's link "
+                                f"bytes as the formula assumes, so no traffic figure is printed"),
+                traffic_raw=cnt.get("raw"))
+
+
+def link_table(mpx, rounds, devs) -> dict:
+    """mpx_link_info for EVERY pair the rounds cover:
+    "g1>g0" -> {type, hops, gpus}; pairs that are not one xGMI hop are listed
+    under "not_one_xgmi_hop" (their rate is not a single link's)."""
+    table, odd = {}, []
+    for rd in range(len(rounds)):
+        for r in range(len(devs)):
+            g, peer = round_role(rounds, rd, r)
+            if g != 1:
+                continue
+            key = f"{r}>{peer}"
+            try:
+                info = dict(mpx.link_info(devs[r], devs[peer]), gpus=[devs[r], devs[peer]], round=rd)
+            except Exception as e:  # noqa: BLE001
+                info = dict(error=f"{type(e).__name__}: {e}"[:160], gpus=[devs[r], devs[peer]], round=rd)
+            table[key] = info
+            if info.get("type") != "xgmi" or info.get("hops") != 1:
+                odd.append(key)
+    return dict(pairs=dict(sorted(table.items(), key=lambda kv: tuple(int(x) for x in kv[0].split(">")))),
+                not_one_xgmi_hop=odd)
 
 
 def pair_latency(mpx, torch, dist, c, rounds, rank, world, tx, rx, errs) -> dict:
@@ -1191,6 +1302,11 @@ def main() -> None:
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(nbytes, 16, 6) if one else cpu_baseline_pairs(world, nbytes, iters, 6)
+        # BASELINE config 1 itself (the reference's 2-rank ping-pong at 8 B
+        # and 4 MiB) beside every line, whatever the workload
+        pp = cpu_baseline_pingpong()
+        if cpu is not None and pp is not None:
+            cpu["config1_pingpong"] = pp
 
     import torch
     import mpx
@@ -1344,10 +1460,7 @@ def main() -> None:
         # local-DRAM figure carries the pushes.
         cnt = res.get("counters")
         if cnt and "error" not in cnt:
-            roof["traffic"] = cnt["link_bytes_per_launch"]
-            roof["traffic_local_dram"] = cnt["local_dram_write_bytes_per_launch"]
-            roof["traffic_source"] = ("xGMI link bytes per G1 launch: (TCC_EA0_WRREQ - TCC_EA0_WRREQ_DRAM) x 64 B of "
-                                      "every GPU, summed; " + cnt["source"])
+            roof.update(link_traffic(cnt))
             extras["counters"] = cnt
         else:
             roof["traffic_source"] = "not measured: " + ((cnt or {}).get("error") or prof_note or "no counter pass")
@@ -1378,13 +1491,10 @@ def main() -> None:
         extras["pair_unidir_GBps"] = res.get("pair_GBps")
         extras["pair_unidir_GBps_min_max"] = res.get("pair_GBps_min_max")
         extras["round_aggregate_GBps"] = res.get("round_aggregate_GBps")
-        peer0 = round_role(all_pairs_rounds(world), 0, 0)[1]
-        if rank == 0 and not os.environ.get("MPX_BENCH_ONE_GPU") and torch.cuda.device_count() > max(dev, peer0):
-            # the path round 0's first pair takes (one process per GPU: local rank = GPU)
-            try:
-                extras["link_round0_pair0"] = dict(mpx.link_info(dev, peer0), gpus=[dev, peer0])
-            except Exception as e:  # noqa: BLE001
-                extras["link_round0_pair0"] = f"{type(e).__name__}: {e}"[:200]
+        if rank == 0 and not os.environ.get("MPX_BENCH_ONE_GPU") and torch.cuda.device_count() >= world:
+            # the path every pair of the steps takes (one process per GPU:
+            # local rank = GPU), so the first node run describes itself
+            extras["link_table"] = link_table(mpx, all_pairs_rounds(world), list(range(world)))
         if "pingpong_8B_half_rtt_us" in res:
             extras["pingpong_8B_half_rtt_us"] = res["pingpong_8B_half_rtt_us"]
             extras["pair_pingpong_8B_half_rtt_us"] = res["pair_pingpong_8B_half_rtt_us"]
@@ -1417,6 +1527,11 @@ def main() -> None:
             tg["pingpong_8B_half_rtt_us"] = dict(value=v, target=f"< {TARGET_HALF_RTT_US} us",
                                                  meets=v < TARGET_HALF_RTT_US)
         tg["all_pairs_aggregate_GBps"] = dict(value=round(value, 3), n_gpus=world, target="reported at 2/4/8 GPUs")
+        lt = extras.get("link_table")
+        if lt is not None:
+            # the targets are per link: a pair that is not one xGMI hop is
+            # named, and its rate is not a single link's
+            tg["pairs_not_one_xgmi_hop"] = lt["not_one_xgmi_hop"]
         if os.environ.get("MPX_BENCH_ONE_GPU"):
             # every rank on GPU 0: loopback pairs, no xGMI link was measured
             for t in tg.values():

@@ -55,6 +55,13 @@ class FakeMpx:
         return "0000:00:00.0" if scenario in ("one_gpu", "rccl_one_gpu") else f"0000:{rank + 1:02x}:00.0"
 
     @staticmethod
+    def link_info(a, b):
+        # every pair one xGMI hop, except GPUs 1 and 2 (two hops): the table
+        # must name it
+        FakeMpx.log.append(["link_info", a, b])
+        return {"type": "xgmi", "hops": 2 if {a, b} == {1, 2} else 1}
+
+    @staticmethod
     def shutdown():
         FakeMpx.log.append(["shutdown"])
 
@@ -145,7 +152,9 @@ class FakeProf:
     """Stand-in for mpx/counters.py: every pass reports fixed counts per
     counter name (per sampling rank), so the aggregation is checkable."""
     COUNTS = {"TCC_EA0_WRREQ_sum": 1000.0, "TCC_EA0_WRREQ_64B_sum": 1000.0, "TCC_EA0_WRREQ_DRAM_sum": 10.0,
-              "TCC_EA0_RDREQ_sum": 50.0, "TCC_EA0_RDREQ_DRAM_sum": 5.0}
+              "TCC_EA0_RDREQ_sum": 50.0, "TCC_EA0_RDREQ_DRAM_sum": 5.0,
+              "TCC_EA0_WRREQ_WRITE_GMI_32B_sum": 1980.0, "TCC_EA0_WRREQ_WRITE_IO_32B_sum": 0.0,
+              "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum": 20.0}
     passes = []
 
     class Pass:

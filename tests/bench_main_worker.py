@@ -26,6 +26,8 @@ W.FakeMpx.spin = _spin
 sys.modules["mpx"] = W.FakeMpx          # bench.main's `import mpx` gets the stand-in
 torch.cuda.set_device = lambda d: None
 torch.cuda.synchronize = lambda *a: None
+# one GPU per rank (bench.main then describes every pair's link: link_table)
+torch.cuda.device_count = lambda: int(os.environ["WORLD_SIZE"])
 bench.EXTRAS_DEADLINE_S = 5
 sys.argv = ["bench.py"] + sys.argv[2:]
 bench.main()

@@ -261,8 +261,20 @@ def test_link_counters_one_sampler_per_gpu(world, scenario, tmp_path):
         assert cnt["link_bytes_per_launch"] == round(samplers * 990 * 64 / launches, 1)
         assert cnt["local_dram_write_bytes_per_launch"] == round(samplers * 10 * 64 / launches, 1)
         assert cnt["link_over_algorithmic"] == round(samplers * 990 * 64 / (n * iters * launches), 5)
+        assert cnt["gmi_write_bytes_per_launch"] == round(samplers * 1980 * 32 / launches, 1)
+        assert cnt["ranks_on_distinct_gpus"] == (scenario != "one_gpu")
+        assert cnt["raw"]["TCC_EA0_WRREQ_sum"] == samplers * 1000.0
+        # the stand-in's 990 link requests are 1.1-4.4 x the pushed bytes here:
+        # on distinct GPUs the self-check refuses the figure; sharing a GPU
+        # no check applies
+        roof = bench.link_traffic(cnt)
+        if scenario == "one_gpu":
+            assert roof["traffic"] == cnt["link_bytes_per_launch"] and roof["traffic_check"].startswith("not applicable")
+        else:
+            assert roof["traffic"] is None and roof["traffic_check"] == "failed"
+            assert "self-check failed" in roof["traffic_reason"] and roof["traffic_raw"] == cnt["raw"]
         sampled = d["rank"] < samplers
-        assert len(d["passes"]) == (2 if sampled else 0)
+        assert len(d["passes"]) == (3 if sampled else 0)
         # each pass wraps exactly one untimed run of every round, after the timed steps
         log = d["log"]
         if sampled:
@@ -272,6 +284,26 @@ def test_link_counters_one_sampler_per_gpu(world, scenario, tmp_path):
                 inside = [x for x in log[i:j] if x[0] == "xfer"]
                 assert len(inside) == world - 1 and all((x[2], x[6], x[7], x[8]) == (2, iters, n, False)
                                                         for x in inside)
+
+
+def test_link_traffic_self_check_band():
+    """bench.link_traffic on distinct GPUs: the subtraction's link bytes
+    inside [0.9, 1.1] x the pushed bytes give the traffic figure; outside
+    (a counter that sees ~0, or too much) the line prints null with the raw
+    counters and the reason; sharing a GPU no check applies."""
+    base = dict(link_bytes_per_launch=1000.0, local_dram_write_bytes_per_launch=5.0, source="src",
+                gmi_over_algorithmic=1.0, io_over_algorithmic=0.0, local_dram_over_algorithmic=0.005,
+                raw={"TCC_EA0_WRREQ_sum": 1.0})
+    for r, ok in ((0.9, True), (1.0, True), (1.1, True), (0.0, False), (0.002, False), (0.89, False), (1.2, False)):
+        roof = bench.link_traffic(dict(base, link_over_algorithmic=r, ranks_on_distinct_gpus=True))
+        if ok:
+            assert roof["traffic"] == 1000.0 and roof["traffic_check"].startswith("passed"), r
+        else:
+            assert roof["traffic"] is None and roof["traffic_check"] == "failed", r
+            assert f"read {r} x" in roof["traffic_reason"] and roof["traffic_raw"] == base["raw"]
+            assert roof["traffic_local_dram"] == 5.0
+    roof = bench.link_traffic(dict(base, link_over_algorithmic=0.0, ranks_on_distinct_gpus=False))
+    assert roof["traffic"] == 1000.0 and roof["traffic_check"].startswith("not applicable")
 
 
 def test_link_counters_need_the_tool_on_every_sampling_rank(tmp_path):

@@ -58,3 +58,13 @@ def test_safe_wall_success_does_not_disarm():
     c, errs = Ctx(), []
     assert bench.safe_wall(c, errs, 2, 1, 0, 1, 10, None, None, 8, barrier=Dist()) == 0.5
     assert c.log == [("xfer", 0)] and not errs
+
+
+def test_config1_pingpong_baseline_shape():
+    """The compiled reference's 2-rank ping-pong (BASELINE config 1) that
+    bench.py puts beside its N = 1 and N >= 2 lines: 8 B half round trip and
+    4 MiB rate, two cores, median of runs 1..5."""
+    pp = bench.cpu_baseline_pingpong()
+    assert pp is not None, "oracle/_ref not built (python -c 'import __graft_entry__ as g; g.build()')"
+    assert pp["cores"] == 2 and pp["kind"] == "reference" and pp["loop"].startswith("ping-pong")
+    assert 0 < pp["half_rtt_us_8B"] < 100 and 0 < pp["GBps_4MiB"] < 1000, pp

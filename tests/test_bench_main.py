@@ -60,9 +60,18 @@ def test_one_json_line_with_the_contract_keys():
     cb = d["cpu_baseline"]
     assert cb["kind"] == "reference" and cb["cores"] == 2 and cb["value"] > 0, cb
     assert "-p 1 -u 1 -b 4194304 -i 500" in cb["sample"]
+    # BASELINE config 1 beside it: the reference's ping-pong at 8 B and 4 MiB
+    pp = cb["config1_pingpong"]
+    assert pp["cores"] == 2 and pp["kind"] == "reference" and "-b 8 -i 20000" in pp["sample"]
+    assert 0 < pp["half_rtt_us_8B"] < 100 and 0 < pp["GBps_4MiB"] < 1000, pp
     # link bytes from the in-process counters (the stand-in's counts: 990
     # link requests of 64 B per sampling rank and pass, 2 samplers, 1 launch)
-    assert d["roofline"]["traffic"] == 2 * 990 * 64 and d["extras"]["counters"]["samplers"] == 2
+    # are 6e-5 x the pushed 4 MiB x 500 on two distinct GPUs: the self-check
+    # prints no traffic figure, with the raw counters and the reason
+    cnt = d["extras"]["counters"]
+    assert cnt["link_bytes_per_launch"] == 2 * 990 * 64 and cnt["samplers"] == 2
+    assert d["roofline"]["traffic"] is None and d["roofline"]["traffic_check"] == "failed"
+    assert d["roofline"]["traffic_raw"]["TCC_EA0_WRREQ_sum"] == 2000.0
     assert d["config"]["ll_max"] == 8192 and d["extras"]["ll_choice"]["chosen_ll_max"] == 8192
     assert d["extras"]["unidir_4MiB_unstaged_GBps"] is not None
     assert d["extras"]["hbv3_rounds_unidir"]["phases_us_median"]["g1"]["kernel_s"] == 1.0
@@ -100,11 +109,19 @@ def test_hung_comparison_engine_cannot_cost_the_line():
 
 def test_every_pair_of_four_ranks_has_a_rate():
     """N = 4, 3 steps = the 3 rounds: all 6 pairs get a G1 launch rate
-    (bytes x iters / that rank's device time) and every round an aggregate."""
+    (bytes x iters / that rank's device time) and every round an aggregate;
+    every pair's link is described (mpx_link_info, the stand-in's GPUs 1-2
+    are two hops apart and named in the targets)."""
     rcs, outs = run("ok", world=4)
     assert rcs == [0] * 4, [o[1][-600:] for o in outs]
     d = lines(outs[0][0])[0]
     e = d["extras"]
+    lt = e["link_table"]
+    assert len(lt["pairs"]) == 6 and {tuple(sorted(v["gpus"])) for v in lt["pairs"].values()} == {
+        (a, b) for a in range(4) for b in range(a + 1, 4)}
+    bad = [k for k, v in lt["pairs"].items() if sorted(v["gpus"]) == [1, 2]]
+    assert lt["not_one_xgmi_hop"] == bad and len(bad) == 1
+    assert e["targets"]["pairs_not_one_xgmi_hop"] == bad
     assert e["pairs_covered"] == 6 and len(e["round_aggregate_GBps"]) == 3
     pairs = {tuple(sorted(map(int, k.split(">")))) for k in e["pair_unidir_GBps"]}
     assert pairs == {(a, b) for a in range(4) for b in range(a + 1, 4)}

@@ -1,0 +1,222 @@
+"""Positive control of bench.py's link-byte counter, on
+one GPU, in-process counters (libmpxprof, mpx/counters.py).
+
+bench.py reads a sender's xGMI bytes as (TCC_EA0_WRREQ - TCC_EA0_WRREQ_DRAM)
+x 64 B: EA write requests NOT destined for local DRAM.  Until now the only
+evidence was ~0 (a loopback pair writes local DRAM).  Here known byte counts
+are written into destinations of every kind one GPU has, by the two writers
+the bench uses, and both counter views are read per case:
+
+  writers       copy  mpx_copy (k_copy: 16-B nontemporal stores), B x iters, into
+                      every destination below
+                push  k_xfer unidir, rank 0 pushes B x iters into rank 1's rx, both
+                      ranks in this process (rx must be an mpx_alloc base: device only)
+  destinations  device           hipMalloc on this GPU (local DRAM: the control's zero)
+                uncached         hipExtMallocWithFlags(hipDeviceMallocUncached)
+                host_coherent    hipHostMalloc(hipHostMallocCoherent): system memory over PCIe
+                host_noncoherent hipHostMalloc(hipHostMallocNonCoherent)
+                ipc_import       this GPU's hipMalloc, opened with hipIpcOpenMemHandle in a
+                                 second process that writes it (copy writer)
+  passes        A  TCC_EA0_WRREQ_sum, TCC_EA0_WRREQ_64B_sum, TCC_EA0_WRREQ_DRAM_sum
+                B  TCC_EA0_WRREQ_WRITE_GMI_32B_sum, _WRITE_IO_32B_sum, _WRITE_DRAM_32B_sum
+
+Per case: subtraction_over_algorithmic = (WRREQ - WRREQ_DRAM) x 64 / bytes,
+gmi / io / dram_over_algorithmic = the 32-B counters x 32 / bytes.  Prints
+one JSON document (profiles/r05_link_counter_control.json).
+
+    python3 tools/link_counter_control.py
+    python3 tools/link_counter_control.py child <handle-hex> <bytes> <iters>   (internal)
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
+
+from mpx import counters  # noqa: E402  (no HIP yet)
+
+PASS_A = ["TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum", "TCC_EA0_WRREQ_DRAM_sum"]
+PASS_B = ["TCC_EA0_WRREQ_WRITE_GMI_32B_sum", "TCC_EA0_WRREQ_WRITE_IO_32B_sum", "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum"]
+B = 16 << 20
+ITERS = 8
+
+hipHostMallocCoherent = 0x40000000
+hipHostMallocNonCoherent = 0x80000000
+hipDeviceMallocUncached = 0x3
+
+
+class IpcHandle(C.Structure):
+    _fields_ = [("reserved", C.c_char * 64)]
+
+
+def hip():
+    h = C.CDLL("libamdhip64.so.7")
+    for name, args in (("hipHostMalloc", [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]),
+                       ("hipHostFree", [C.c_void_p]),
+                       ("hipExtMallocWithFlags", [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]),
+                       ("hipMalloc", [C.POINTER(C.c_void_p), C.c_size_t]),
+                       ("hipFree", [C.c_void_p]),
+                       ("hipIpcGetMemHandle", [C.POINTER(IpcHandle), C.c_void_p]),
+                       ("hipIpcOpenMemHandle", [C.POINTER(C.c_void_p), IpcHandle, C.c_uint]),
+                       ("hipIpcCloseMemHandle", [C.c_void_p]),
+                       ("hipDeviceSynchronize", [])):
+        f = getattr(h, name)
+        f.restype, f.argtypes = C.c_int, args
+    return h
+
+
+def ck(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: hip error {rc}")
+
+
+def passes(bus, work):
+    """run work() once per pass; returns {counter: value}"""
+    vals = {}
+    for names in (PASS_A, PASS_B):
+        with counters.Pass(bus, names) as p:
+            work()
+        vals.update(zip(names, p.values))
+    return vals
+
+
+def summarise(vals, nbytes):
+    wr, w64, dram = (vals[k] for k in PASS_A)
+    gmi, io, dram32 = (vals[k] for k in PASS_B)
+    return dict(algorithmic_bytes=nbytes, counters=vals,
+                subtraction_over_algorithmic=round((wr - dram) * 64 / nbytes, 5),
+                write_requests_64B_fraction=round(w64 / wr, 5) if wr else None,
+                gmi_over_algorithmic=round(gmi * 32 / nbytes, 5),
+                io_over_algorithmic=round(io * 32 / nbytes, 5),
+                dram_over_algorithmic=round(dram32 * 32 / nbytes, 5))
+
+
+def child(handle_hex, nbytes, iters):
+    counters.register()
+    import mpx
+    H = hip()
+    mpx.device_count()
+    bus = mpx.bus_id(0)
+    h = IpcHandle()
+    C.memmove(C.addressof(h), bytes.fromhex(handle_hex), 64)
+    p = C.c_void_p()
+    ck(H.hipIpcOpenMemHandle(C.byref(p), h, 1), "hipIpcOpenMemHandle")
+    with mpx.Context(1, "kernel") as c:
+        src = c.alloc(0, nbytes)
+        c.fill(src, nbytes, mpx.FILL_SPLITMIX, 3)
+        dst = mpx.Buffer(p.value, 0, nbytes)
+        c.copy(0, dst, src, nbytes, 1)
+        vals = passes(bus, lambda: c.copy(0, dst, src, nbytes, iters))
+        ok = c.checksum(dst, nbytes) == c.checksum(src, nbytes)
+        c.free(src)
+    ck(H.hipIpcCloseMemHandle(p), "hipIpcCloseMemHandle")
+    print(json.dumps(dict(summarise(vals, nbytes * iters), copy_checked=ok)))
+
+
+def main():
+    try:
+        counters.register()
+        reg = "ok"
+    except counters.CounterError as e:
+        reg = str(e)
+    import mpx
+    H = hip()
+    mpx.device_count()
+    out = dict(tool="tools/link_counter_control.py", register=reg, ready=counters.ready(), bytes=B, iters=ITERS,
+               formula="bench.py link bytes = (TCC_EA0_WRREQ - TCC_EA0_WRREQ_DRAM) x 64", cases={})
+    if not counters.ready():
+        out["error"] = counters.error()
+        print(json.dumps(out))
+        return 1
+    bus = mpx.bus_id(0)
+    out["bus"] = bus
+
+    def dest(kind):
+        p = C.c_void_p()
+        if kind == "host_coherent":
+            ck(H.hipHostMalloc(C.byref(p), B, hipHostMallocCoherent), "hipHostMalloc coherent")
+            return p.value, lambda: H.hipHostFree(p)
+        if kind == "host_noncoherent":
+            ck(H.hipHostMalloc(C.byref(p), B, hipHostMallocNonCoherent), "hipHostMalloc noncoherent")
+            return p.value, lambda: H.hipHostFree(p)
+        if kind == "uncached":
+            ck(H.hipExtMallocWithFlags(C.byref(p), B, hipDeviceMallocUncached), "hipExtMallocWithFlags")
+            return p.value, lambda: H.hipFree(p)
+        ck(H.hipMalloc(C.byref(p), B), "hipMalloc")
+        return p.value, lambda: H.hipFree(p)
+
+    with mpx.Context(2, "kernel") as c:
+        src, src1, rx0 = c.alloc(0, B), c.alloc(0, B), c.alloc(0, B)
+        c.fill(src, B, mpx.FILL_SPLITMIX, 1)
+        c.fill(src1, B, mpx.FILL_SPLITMIX, 2)
+        for kind in ("device", "uncached", "host_coherent", "host_noncoherent"):
+            ptr, release = dest(kind)
+            dst = mpx.Buffer(ptr, 0, B)
+            try:
+                c.copy(0, dst, src, B, 1)
+                t0 = time.perf_counter()
+                vals = passes(bus, lambda: c.copy(0, dst, src, B, ITERS))
+                case = summarise(vals, B * ITERS)
+                case["copy_checked"] = c.checksum(dst, B) == c.checksum(src, B)
+                case["pass_s"] = round(time.perf_counter() - t0, 3)
+                out["cases"][f"copy->{kind}"] = case
+            except Exception as e:  # noqa: BLE001
+                out["cases"][f"*->{kind}"] = f"{type(e).__name__}: {e}"
+            finally:
+                ck(H.hipDeviceSynchronize(), "hipDeviceSynchronize")
+                release()
+        # push: rank 0 pushes B x ITERS into rank 1's rx (an mpx_alloc base on
+        # this GPU: attach takes no other kind), both ranks in this process
+        c.attach(0, 0, src, rx0, B)
+        rx1 = c.alloc(0, B)
+        c.attach(1, 0, src1, rx1, B)
+        errs = []
+
+        def side(r):
+            try:
+                c.xfer(mpx.MODE_UNIDIR, 1 if r == 0 else 0, r, 1 - r, ITERS, src if r == 0 else src1,
+                       rx0 if r == 0 else rx1, B, timeout_ms=20000)
+            except Exception as e:  # noqa: BLE001
+                errs.append(f"rank {r}: {e}")
+
+        def push():
+            th = [threading.Thread(target=side, args=(r,)) for r in (0, 1)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+
+        push()
+        case = summarise(passes(bus, push), B * ITERS)
+        case["push_checked"] = c.checksum(rx1, B) == c.checksum(src, B)
+        case["errors"] = errs
+        out["cases"]["push->device"] = case
+        # ipc_import: this process's allocation, written by a second process that opened it
+        ipc = c.alloc(0, B)
+        h = IpcHandle()
+        ck(H.hipIpcGetMemHandle(C.byref(h), C.c_void_p(ipc.ptr)), "hipIpcGetMemHandle")
+        r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "child",
+                            C.string_at(C.addressof(h), 64).hex(), str(B), str(ITERS)],
+                           capture_output=True, text=True, timeout=150)
+        try:
+            out["cases"]["copy->ipc_import"] = json.loads(r.stdout.strip().splitlines()[-1])
+            out["cases"]["copy->ipc_import"]["copy_checked_by_owner"] = c.checksum(ipc, B) == c.checksum(src, B)
+        except Exception:  # noqa: BLE001
+            out["cases"]["copy->ipc_import"] = f"child rc {r.returncode}: {r.stderr[-400:]}"
+        for b in (ipc,):
+            c.free(b)
+    mpx.shutdown()
+    print(json.dumps(out, indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "child":
+        child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
+    else:
+        sys.exit(main())
