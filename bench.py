@@ -55,11 +55,12 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-perf_amd"))
 from mpx.schedule import all_pairs_rounds, round_role  # noqa: E402  (pure Python, no GPU)
 
 HBM_PEAK_GBPS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# xGMI: BASELINE.json quotes ~153 GB/s per link.  That is the link's
-# bidirectional figure (MI355X: 7 links x 153.6 GB/s = 1075 GB/s aggregate
-# peer bandwidth, both directions counted), i.e. 76.8 GB/s per direction.  A
-# unidirectional pair uses one direction of its one link, so that is its
-# roofline; the bidirectional figure is reported beside it.
+# xGMI: BASELINE.json quotes ~153 GB/s per link.  Read here as the link's
+# two directions summed (AMD's datasheet convention, from memory: 153.6 GB/s
+# per link, 7 links; x16 at 38.4 Gb/s per lane = 76.8 GB/s each way — not
+# verifiable offline).  A unidirectional pair uses one
+# direction of its one link, so 76.8 is its roofline; the fraction against
+# 153.6 is reported beside it, and the targets carry both verdicts.
 XGMI_LINK_PEAK_BIDIR_GBPS = 153.6
 XGMI_LINK_PEAK_GBPS = XGMI_LINK_PEAK_BIDIR_GBPS / 2
 # north_star's targets (BASELINE.json): per-pair unidirectional bandwidth
