@@ -8,10 +8,13 @@ import ctypes as C
 import os
 import shutil
 import subprocess
+import sys
 
 import pytest
 
 import mpx
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -147,3 +150,30 @@ int main() {
                    check=True, capture_output=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
     assert out == ["64", "64", "0", "56", "1", "1"], out
+
+
+@pytest.mark.parametrize("torch_first", [False, True])
+def test_rccl_is_the_images_whatever_was_loaded_first(torch_first):
+    """libmpx binds RCCL at run time from /opt/rocm/lib/librccl.so.1
+    (RTLD_LOCAL | RTLD_DEEPBIND), so a process that imported torch first
+    (its bundled librccl.so.1 2.26.6 loaded) still runs the image's RCCL,
+    as mpx_perf does.  No GPU call: ncclGetVersion."""
+    code = ("import sys, json; sys.path.insert(0, %r)\n" % os.path.join(os.path.dirname(HERE), "mpi-perf_amd")
+            + ("import torch\n" if torch_first else "")
+            + "import mpx; print(json.dumps(mpx.rccl_version()))")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-600:]
+    import json
+    v = json.loads(r.stdout.strip().splitlines()[-1])
+    assert v["library"] == "/opt/rocm/lib/librccl.so.1" and v["release"].startswith("2.27"), v
+
+
+def test_rccl_unloadable_is_an_error_not_a_fallback(tmp_path):
+    """MPX_RCCL_LIB naming a file that cannot be loaded: the RCCL entry points
+    fail with MPX_ERR_RCCL and the loader's message."""
+    code = ("import sys; sys.path.insert(0, %r)\n" % os.path.join(os.path.dirname(HERE), "mpi-perf_amd")
+            + "import mpx\ntry:\n    mpx.rccl_version()\nexcept mpx.MpxError as e:\n"
+            + "    print(e.status == mpx.ERR_RCCL, 'cannot load' in str(e))\n")
+    env = dict(os.environ, MPX_RCCL_LIB=str(tmp_path / "nope.so"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.stdout.split() == ["True", "True"], (r.stdout, r.stderr[-400:])
