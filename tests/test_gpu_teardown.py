@@ -1,0 +1,48 @@
+"""Stream teardown mid-process (round 5, DESIGN.md §5 "Exit").
+
+Rounds 2-4 could not destroy CU-masked rank streams while the process ran:
+the destroy raced HIP's completion handler of the stream's last command,
+whose release then ran the queue's destruction on the HSA events thread,
+which deadlocked on itself (profiles/r05_exit_stall_symbolized.txt).
+callback_fence now waits for that handler (event_thread_barrier), so
+mpx_shutdown can destroy the pooled rank streams between contexts, every
+time, and the next context creates fresh ones.  Each case runs in a child
+process under a time limit: a stall ends the child, not the suite."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CYCLES = """
+import sys, threading
+sys.path.insert(0, {pkg!r}); sys.path.insert(0, {here!r})
+import mpx
+from pairs import Pairs
+for k in range({n}):
+    P = Pairs({engine!r}, {npairs}, 1 << 16, fill="seeded")
+    try:
+        out, errs = P.run(mpx.MODE_PINGPONG, 4096, 3)
+        assert not errs, errs
+        assert all(o.check_failures == 0 for o in out.values())
+    finally:
+        P.close()
+    mpx.shutdown()   # every rank stream destroyed; the next cycle creates new ones
+print("cycles done", {n}, flush=True)
+"""
+
+
+@pytest.mark.parametrize("engine,npairs", [("kernel", 1), ("kernel", 2), ("sdma", 1)])
+def test_rank_streams_destroyed_and_recreated_every_cycle(engine, npairs):
+    """30 cycles of: a context with 2 x npairs ranks on GPU 0, a checked
+    ping-pong on every pair, finalize, mpx_shutdown (the rank streams are
+    destroyed), in ONE process; then the process exits normally."""
+    code = CYCLES.format(pkg=os.path.join(os.path.dirname(HERE), "mpi-perf_amd"), here=HERE, n=30, engine=engine,
+                         npairs=npairs)
+    r = subprocess.run([sys.executable, "-u", "-c", code], capture_output=True, text=True, timeout=100,
+                       env=dict(os.environ))
+    assert r.returncode == 0 and "cycles done 30" in r.stdout, (r.returncode, r.stdout[-400:], r.stderr[-800:])
