@@ -43,11 +43,13 @@ step_ok() {  # name rc
 }
 
 rehearse() {
-    local n=$1
+    local n=$1 t0=$SECONDS
     MPX_BENCH_ONE_GPU=1 timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
         --master-addr 127.0.0.1 --master-port $((29520 + n + RANDOM % 200)) bench.py --gpus $n \
         > $O/bench_n$n.json 2> $O/bench_n$n.err
-    step_ok rehearse$n $?
+    local rc=$?
+    echo "rehearse$n: $((SECONDS - t0)) s"
+    step_ok rehearse$n $rc
 }
 
 procs_exit() {  # K runs of the processes-mode pingpong; a run whose ranks do not end is SIGUSR1'd (stacks) then killed
