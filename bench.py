@@ -1050,6 +1050,11 @@ def pairs_bench(mpx, torch, dist, engine, rank, world, dev, nbytes, iters, steps
             return g, t
         except Exception as e:  # noqa: BLE001
             step_err.append(f"rank {rank}: step {s}: {type(e).__name__}: {e}"[:300])
+            if armed:   # the start never came (a failed barrier): cancel the armed kernel now
+                try:
+                    c.disarm(rank)
+                except Exception:  # noqa: BLE001
+                    pass
             return g, None
 
     # SDMA engine: its graph-captured chunks are built for every round's
