@@ -192,7 +192,9 @@ int mpx_finalize(mpx_ctx *ctx);
 /* After the last mpx_finalize: destroy the process-lifetime rank streams
    (mpx_finalize returns them to a per-device pool) while the process is
    fully alive, instead of leaving them to the HIP runtime's exit teardown.
-   MPX_ERR_STATE while a context is alive. */
+   MPX_ERR_STATE while a context is alive; MPX_ERR_TIMEOUT (streams left to
+   the runtime) if the stream fence did not complete in 10 s.  May be called
+   mid-process: a later context creates new rank streams. */
 int mpx_shutdown(void);
 
 /* ---- buffers (allocate_tx_rx_buffers, mpi_perf.c:240-252) ---------------- */
