@@ -259,7 +259,12 @@ int mpx_xfer_ex(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank
    kernel's whole grid runs and waits (at most 5 ms later), so the start does
    not also pay the rest of the dispatch.  A rank holds one armed call;
    mpx_xfer_ex with other arguments fails (MPX_ERR_STATE) and leaves it
-   armed.  The SDMA and RCCL engines accept the call and do nothing. */
+   armed.  An armed kernel waits for its start at most max(the call's
+   timeout, 60 s) — the host's barrier lies between arm and start — and
+   then ends the call with MPX_ERR_TIMEOUT; a host whose start will not
+   come (a failed barrier) cancels it with mpx_xfer_disarm at once.  A
+   failed arm leaves the link as it was (no call number taken).  The SDMA
+   and RCCL engines accept the call and do nothing. */
 int mpx_xfer_arm(mpx_ctx *ctx, int mode, int my_group, int my_rank, int peer_rank, int iters,
                  void *tx, void *rx, int buff_len, const mpx_xfer_opts *opts);
 /* Cancel an armed call that will not be started (no transfer happens);
