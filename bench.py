@@ -773,6 +773,81 @@ FABRIC_COUNTERS = ("TCC_EA0_WRREQ_WRITE_GMI_32B_sum", "TCC_EA0_WRREQ_WRITE_IO_32
 LINK_CHECK_BAND = (0.9, 1.1)
 COUNTER_SETS = (LINK_COUNTERS, READ_COUNTERS, FABRIC_COUNTERS)
 ALL_COUNTERS = LINK_COUNTERS + READ_COUNTERS + FABRIC_COUNTERS
+# the candidate link-byte formulas, in order of preference: the EA write
+# requests not destined for local DRAM x 64 B, the GMI-path 32-B writes x 32,
+# the IO-path 32-B writes x 32
+LINK_FORMULAS = ("subtraction", "gmi", "io")
+# peer_link_control: known bytes written across one link by k_copy (not the
+# pair kernel); a formula reading them within this band is validated
+PEER_CONTROL_BYTES, PEER_CONTROL_ITERS, PEER_CONTROL_BAND = 16 << 20, 8, (0.95, 1.1)
+
+
+def link_formula_bytes(v: dict) -> dict:
+    """bytes each candidate link formula reads from one set of counter values"""
+    return dict(subtraction=(v["TCC_EA0_WRREQ_sum"] - v["TCC_EA0_WRREQ_DRAM_sum"]) * 64,
+                gmi=v["TCC_EA0_WRREQ_WRITE_GMI_32B_sum"] * 32,
+                io=v["TCC_EA0_WRREQ_WRITE_IO_32B_sum"] * 32)
+
+
+def peer_link_control(mpx, prof, bus: str, dev: int, peer_dev: int) -> dict:
+    """Positive control of the link-byte counters ON the node, independent
+    of the pair kernel (one GPU can only show host and
+    local destinations: tools/link_counter_control.py).  In this process, a
+    second context with one rank on `dev` and one on `peer_dev` (peer access
+    both ways): k_copy on `dev` writes B x iters known bytes into `peer_dev`'s
+    memory, then the pair kernel pushes B x iters (unidir, threads) the same
+    way; this GPU's counters (LINK_COUNTERS, FABRIC_COUNTERS) are read around
+    each.  The first formula whose copy reading lies in PEER_CONTROL_BAND is
+    the validated one; None if none does."""
+    import threading
+    B, IT = PEER_CONTROL_BYTES, PEER_CONTROL_ITERS
+    out = dict(bytes=B * IT, gpus=[dev, peer_dev], band=list(PEER_CONTROL_BAND),
+               writers="copy: k_copy on gpus[0] into gpus[1]'s HBM; push: k_xfer unidir gpus[0] -> gpus[1]")
+    c = mpx.Context(2, "kernel")
+    try:
+        tx0, rx0, tx1, rx1 = c.alloc(dev, B), c.alloc(dev, B), c.alloc(peer_dev, B), c.alloc(peer_dev, B)
+        c.fill(tx0, B, mpx.FILL_SPLITMIX, 0x11)
+        c.fill(tx1, B, mpx.FILL_SPLITMIX, 0x22)
+        c.attach(0, dev, tx0, rx0, B)
+        c.attach(1, peer_dev, tx1, rx1, B)
+        errs = []
+
+        def copy():
+            c.copy(dev, rx1, tx0, B, IT)
+
+        def side(r):
+            try:
+                c.xfer(mpx.MODE_UNIDIR, 1 - r, r, 1 - r, IT, (tx0, tx1)[r], (rx0, rx1)[r], B, timeout_ms=5000)
+            except Exception as e:  # noqa: BLE001
+                errs.append(f"{type(e).__name__}: {e}"[:160])
+
+        def push():
+            th = [threading.Thread(target=side, args=(r,)) for r in (0, 1)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+
+        for name, work in (("copy", copy), ("push", push)):
+            work()
+            vals = {}
+            for names in (LINK_COUNTERS, FABRIC_COUNTERS):
+                with prof.Pass(bus, list(names)) as p:
+                    work()
+                vals.update(zip(names, p.values))
+            fb = link_formula_bytes(vals)
+            out[name] = dict({f"{k}_over_bytes": round(v / (B * IT), 5) for k, v in fb.items()},
+                             dram_over_bytes=round(vals["TCC_EA0_WRREQ_WRITE_DRAM_32B_sum"] * 32 / (B * IT), 5),
+                             raw=vals)
+        out["copy_checked"] = c.checksum(rx1, B) == c.checksum(tx0, B)
+        if errs:
+            out["push_errors"] = errs
+    finally:
+        c.close()
+    lo, hi = PEER_CONTROL_BAND
+    out["validated_formula"] = next((f for f in LINK_FORMULAS
+                                     if out["copy_checked"] and lo <= out["copy"][f"{f}_over_bytes"] <= hi), None)
+    return out
 
 
 def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes, iters, nwg, stream, buses,
@@ -830,6 +905,7 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
     distinct = len(set(buses)) == world
     g1_avg = sum(float(e[-2]) for e in every) / max(sum(float(e[-1]) for e in every), 1.0)
     link = (wr - dram) * 64
+    formulas = link_formula_bytes(dict(zip(ALL_COUNTERS, tot)))
     out = dict(
         source="in-process rocprofiler-sdk device counting service (mpi-perf_amd/lib/libmpxprof.so), one pass per "
                "counter set over an untimed re-run of every round (the timed steps' loop, width and hint), one "
@@ -847,9 +923,23 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
         g1_avg_launch_us=round(g1_avg * 1e6, 2),
         achieved_link_GBps_per_pair=round(link / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
         achieved_local_dram_GBps_per_pair=round(dram * 64 / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
-        reads_reset=vals.get("reads_reset"))
+        reads_reset=vals.get("reads_reset"),
+        link_formula_bytes_per_launch={k: round(v / launches, 1) for k, v in formulas.items()},
+        link_formula_over_algorithmic={k: round(v / alg, 5) for k, v in formulas.items()})
     if notes:
         out["notes"] = notes
+    if distinct:
+        # rank 0 validates the formulas on this node with known bytes across
+        # its round-0 link, while the other ranks wait (untimed)
+        if rank == 0:
+            peer = round_role(rounds, 0, 0)[1]
+            try:
+                peer_dev = next(d for d in range(mpx.device_count()) if mpx.bus_id(d) == buses[peer])
+                my_dev = next(d for d in range(mpx.device_count()) if mpx.bus_id(d) == buses[rank])
+                out["peer_control"] = peer_link_control(mpx, prof, buses[rank], my_dev, peer_dev)
+            except Exception as e:  # noqa: BLE001
+                out["peer_control"] = {"error": f"{type(e).__name__}: {e}"[:240]}
+        dist.barrier()
     return out
 
 
@@ -870,6 +960,20 @@ def link_traffic(cnt: dict) -> dict:
     if not cnt.get("ranks_on_distinct_gpus"):
         return dict(traffic=cnt["link_bytes_per_launch"], traffic_local_dram=cnt["local_dram_write_bytes_per_launch"],
                     traffic_source=src, traffic_check="not applicable: ranks share a GPU (local pushes, ~0 expected)")
+    pc = cnt.get("peer_control") or {}
+    f = pc.get("validated_formula")
+    if f:
+        # a formula validated on THIS node by known bytes across a link (an
+        # independent writer): it measures the pushes, whatever they read
+        fr = cnt["link_formula_over_algorithmic"][f]
+        return dict(traffic=cnt["link_formula_bytes_per_launch"][f],
+                    traffic_local_dram=cnt["local_dram_write_bytes_per_launch"],
+                    traffic_source=f"xGMI link bytes per G1 launch by the '{f}' formula, validated on this node: "
+                                   f"{pc['copy'][f + '_over_bytes']} x the bytes k_copy wrote across a link "
+                                   f"(extras.counters.peer_control); " + cnt["source"],
+                    traffic_check=(f"validated ({f}); the pushes read {fr} x the pushed bytes" +
+                                   ("" if lo <= fr <= hi else f" — outside {lo}-{hi}: link bytes differ from the "
+                                                              f"pushed bytes")))
     if lo <= r <= hi:
         return dict(traffic=cnt["link_bytes_per_launch"], traffic_local_dram=cnt["local_dram_write_bytes_per_launch"],
                     traffic_source=src, traffic_check=f"passed: link bytes {r} x the pushed bytes (band {lo}-{hi})")
@@ -878,8 +982,10 @@ def link_traffic(cnt: dict) -> dict:
                 traffic_reason=(f"link-byte self-check failed: (WRREQ - WRREQ_DRAM) x 64 read {r} x the pushed bytes "
                                 f"(band {lo}-{hi}); the GMI 32-B write counter reads {cnt.get('gmi_over_algorithmic')}, "
                                 f"IO {cnt.get('io_over_algorithmic')}, local DRAM "
-                                f"{cnt.get('local_dram_over_algorithmic')} x: the counters do not see this path's link "
-                                f"bytes as the formula assumes, so no traffic figure is printed"),
+                                f"{cnt.get('local_dram_over_algorithmic')} x; the peer control validated no formula "
+                                f"({(cnt.get('peer_control') or {}).get('error') or 'see extras.counters.peer_control'})"
+                                f": the counters do not see this path's link bytes as the formula assumes, so no "
+                                f"traffic figure is printed"),
                 traffic_raw=cnt.get("raw"))
 
 

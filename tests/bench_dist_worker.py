@@ -51,8 +51,16 @@ class FakeMpx:
 
     @staticmethod
     def bus_id(dev):
-        # one GPU per rank, unless the scenario puts every rank on one card
-        return "0000:00:00.0" if scenario in ("one_gpu", "rccl_one_gpu") else f"0000:{rank + 1:02x}:00.0"
+        # one GPU per rank, unless the scenario puts every rank on one card;
+        # every rank passes dev 0 for its own GPU, and another device index d
+        # is GPU d (rank d's card) — rank 0's peer control looks its peer up
+        if scenario in ("one_gpu", "rccl_one_gpu"):
+            return "0000:00:00.0"
+        return f"0000:{(rank if dev == 0 else dev) + 1:02x}:00.0"
+
+    @staticmethod
+    def device_count():
+        return world
 
     @staticmethod
     def link_info(a, b):
@@ -81,6 +89,9 @@ class FakeMpx:
 
         def fill(self, b, n, pattern, key):
             self.filled = key
+
+        def copy(self, dev, dst, src, n, iters):
+            FakeMpx.log.append(["copy", dev, dst[1], src[1], n, iters])
 
         def attach(self, r, dev, tx, rx, n):
             FakeMpx.log.append(["attach", r, dev, n])
@@ -198,6 +209,10 @@ if __name__ == "__main__":
     rank, world, port, scenario, outdir = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4],
                                            sys.argv[5])
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    if scenario == "counters_validated":
+        # the GMI counter reads exactly the peer control's known bytes per pass
+        FakeProf.COUNTS["TCC_EA0_WRREQ_WRITE_GMI_32B_sum"] = float(bench.PEER_CONTROL_BYTES * bench.PEER_CONTROL_ITERS
+                                                                   // 32)
     extras = {}
     out = {"rank": rank}
     try:
@@ -208,9 +223,9 @@ if __name__ == "__main__":
         else:
             # one_gpu: only rank 0 registers the tool (bench.main's one-GPU
             # rehearsal); counters_missing: sampling rank 1 has none
-            prof = FakeProf if (scenario == "counters" or (scenario == "one_gpu" and rank == 0)
+            prof = FakeProf if (scenario in ("counters", "counters_validated") or (scenario == "one_gpu" and rank == 0)
                                 or (scenario == "counters_missing" and rank != 1)) else None
-            count = scenario in ("counters", "one_gpu", "counters_missing")
+            count = scenario in ("counters", "counters_validated", "one_gpu", "counters_missing")
             # the per-round barriers spin in shared memory, as in bench.main (world 2 and 4 here)
             d, spin = bench.spin_barrier_dist(dist, rank, world) if scenario == "ok" else (dist, None)
             out["spin"] = spin is not None

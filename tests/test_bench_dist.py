@@ -274,12 +274,23 @@ def test_link_counters_one_sampler_per_gpu(world, scenario, tmp_path):
             assert roof["traffic"] is None and roof["traffic_check"] == "failed"
             assert "self-check failed" in roof["traffic_reason"] and roof["traffic_raw"] == cnt["raw"]
         sampled = d["rank"] < samplers
-        assert len(d["passes"]) == (3 if sampled else 0)
+        # rank 0 adds the peer control's passes on distinct GPUs: two writers x
+        # two counter sets (its bytes are unrelated to the stand-in's counts, so
+        # it validates no formula here)
+        extra = 4 if (d["rank"] == 0 and scenario != "one_gpu") else 0
+        assert len(d["passes"]) == (3 if sampled else 0) + extra
+        if d["rank"] == 0 and scenario != "one_gpu":
+            pc = cnt["peer_control"]
+            peer = round_role(all_pairs_rounds(world), 0, 0)[1]
+            assert pc["gpus"] == [0, peer] and pc["validated_formula"] is None, pc
+            assert ["copy", 0, peer, 0, bench.PEER_CONTROL_BYTES, bench.PEER_CONTROL_ITERS] in d["log"]
+        else:
+            assert "peer_control" not in cnt
         # each pass wraps exactly one untimed run of every round, after the timed steps
         log = d["log"]
         if sampled:
-            b = [i for i, x in enumerate(log) if x[0] == "pass_begin"]
-            e = [i for i, x in enumerate(log) if x[0] == "pass_end"]
+            b = [i for i, x in enumerate(log) if x[0] == "pass_begin"][:3]
+            e = [i for i, x in enumerate(log) if x[0] == "pass_end"][:3]
             for i, j in zip(b, e):
                 inside = [x for x in log[i:j] if x[0] == "xfer"]
                 assert len(inside) == world - 1 and all((x[2], x[6], x[7], x[8]) == (2, iters, n, False)
@@ -304,6 +315,41 @@ def test_link_traffic_self_check_band():
             assert roof["traffic_local_dram"] == 5.0
     roof = bench.link_traffic(dict(base, link_over_algorithmic=0.0, ranks_on_distinct_gpus=False))
     assert roof["traffic"] == 1000.0 and roof["traffic_check"].startswith("not applicable")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_control_validates_a_formula(world, tmp_path):
+    """On distinct GPUs rank 0 writes known bytes across its round-0 link
+    (k_copy into the peer GPU's memory, then a threads-mode push) under the
+    counters; here the stand-in's GMI counter reads exactly those bytes, so
+    the 'gmi' formula is validated and measures the pushes (which, at the
+    stand-in's fixed counts, read far more than the pushed bytes: the line
+    says so)."""
+    res = run(world, "counters_validated", tmp_path)
+    d = next(x for x in res if x["rank"] == 0)
+    cnt = d["res"]["counters"]
+    pc = cnt["peer_control"]
+    assert pc["validated_formula"] == "gmi" and pc["copy"]["gmi_over_bytes"] == 1.0, pc
+    assert pc["copy"]["subtraction_over_bytes"] < 0.01 and pc["copy_checked"] is True
+    roof = bench.link_traffic(cnt)
+    assert roof["traffic"] == cnt["link_formula_bytes_per_launch"]["gmi"]
+    assert roof["traffic_check"].startswith("validated (gmi)") and "outside" in roof["traffic_check"]
+
+
+def test_link_traffic_prefers_a_validated_formula():
+    cnt = dict(link_bytes_per_launch=0.0, local_dram_write_bytes_per_launch=5.0, source="src",
+               link_over_algorithmic=0.0, ranks_on_distinct_gpus=True, gmi_over_algorithmic=1.0,
+               io_over_algorithmic=0.0, local_dram_over_algorithmic=0.0, raw={},
+               link_formula_bytes_per_launch=dict(subtraction=0.0, gmi=1000.0, io=0.0),
+               link_formula_over_algorithmic=dict(subtraction=0.0, gmi=1.001, io=0.0),
+               peer_control=dict(validated_formula="gmi", copy=dict(gmi_over_bytes=0.998)))
+    roof = bench.link_traffic(cnt)
+    assert roof["traffic"] == 1000.0 and roof["traffic_check"] == "validated (gmi); the pushes read 1.001 x the pushed bytes"
+    assert "0.998 x the bytes k_copy wrote across a link" in roof["traffic_source"]
+    # no validated formula: the subtraction's self-check decides (here: fails)
+    cnt["peer_control"] = dict(validated_formula=None)
+    roof = bench.link_traffic(cnt)
+    assert roof["traffic"] is None and roof["traffic_check"] == "failed"
 
 
 def test_link_counters_need_the_tool_on_every_sampling_rank(tmp_path):

@@ -210,6 +210,19 @@ def main():
             out["cases"]["copy->ipc_import"] = f"child rc {r.returncode}: {r.stderr[-400:]}"
         for b in (ipc,):
             c.free(b)
+    # bench.py's on-node control (bench.peer_link_control): known bytes from
+    # GPU 0 into another GPU's HBM when there is one — the destination one
+    # GPU cannot show — else GPU 0 into itself (local DRAM: exercises the
+    # same code, validates nothing)
+    sys.path.insert(0, ROOT)
+    import bench
+    peer = 1 if mpx.device_count() > 1 else 0
+    try:
+        out["peer_link_control"] = dict(bench.peer_link_control(mpx, counters, bus, 0, peer),
+                                        note="GPU 0 -> GPU 1 across xGMI" if peer else
+                                        "one GPU: GPU 0 -> GPU 0 (local DRAM), the code path only")
+    except Exception as e:  # noqa: BLE001
+        out["peer_link_control"] = f"{type(e).__name__}: {e}"[:300]
     mpx.shutdown()
     print(json.dumps(out, indent=1))
     return 0
