@@ -813,7 +813,13 @@ def peer_link_control(mpx, prof, bus: str, dev: int, peer_dev: int) -> dict:
         errs = []
 
         def copy():
-            c.copy(dev, rx1, tx0, B, IT)
+            # a launch per copy: every byte crosses once per launch, and each
+            # launch's end-of-kernel release writes back what the L2 holds —
+            # one launch of IT copies lets a write-back-cached destination
+            # absorb the rewrites in the L2 (tools/link_counter_control.py:
+            # coherent host memory reads 0.39 x that way)
+            for _ in range(IT):
+                c.copy(dev, rx1, tx0, B, 1)
 
         def side(r):
             try:

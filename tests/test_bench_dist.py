@@ -283,7 +283,9 @@ def test_link_counters_one_sampler_per_gpu(world, scenario, tmp_path):
             pc = cnt["peer_control"]
             peer = round_role(all_pairs_rounds(world), 0, 0)[1]
             assert pc["gpus"] == [0, peer] and pc["validated_formula"] is None, pc
-            assert ["copy", 0, peer, 0, bench.PEER_CONTROL_BYTES, bench.PEER_CONTROL_ITERS] in d["log"]
+            copies = [x for x in d["log"] if x[0] == "copy"]
+            # warm-up + two passes, a launch per copy
+            assert copies == [["copy", 0, peer, 0, bench.PEER_CONTROL_BYTES, 1]] * (3 * bench.PEER_CONTROL_ITERS)
         else:
             assert "peer_control" not in cnt
         # each pass wraps exactly one untimed run of every round, after the timed steps
