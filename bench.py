@@ -934,7 +934,9 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
         link_formula_over_algorithmic={k: round(v / alg, 5) for k, v in formulas.items()})
     if notes:
         out["notes"] = notes
-    if distinct:
+    # MPX_BENCH_PEER_CONTROL=1 runs the control on a one-GPU rehearsal too
+    # (GPU 0 -> GPU 0: the integration on hardware; it validates nothing)
+    if distinct or os.environ.get("MPX_BENCH_PEER_CONTROL") == "1":
         # rank 0 validates the formulas on this node with known bytes across
         # its round-0 link, while the other ranks wait (untimed)
         if rank == 0:
