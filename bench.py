@@ -66,42 +66,217 @@ XGMI_LINK_PEAK_GBPS = XGMI_LINK_PEAK_BIDIR_GBPS / 2
 # north_star's targets (BASELINE.json): per-pair unidirectional bandwidth
 # >= 85 % of xGMI link peak at >= 4 MB, device-initiated 8 B latency < 3 us
 TARGET_LINK_FRAC, TARGET_HALF_RTT_US = 0.85, 3.0
+# The bar as SURVEY/BASELINE state it: ~153 GB/s per link PER DIRECTION
+# (SURVEY.md:361; BASELINE.md:51 "~130 of ~153 GB/s") — the primary verdict.
+STATED_LINK_PEAK_GBPS = XGMI_LINK_PEAK_BIDIR_GBPS
+
+
+def link_target(achieved: float, nbytes: int) -> dict:
+    """extras.targets.per_pair_unidir_GBps: `meets` is judged against the
+    stated bar (0.85 x 153.6 GB/s per direction, SURVEY.md:361); the
+    per-direction reading of 153.6 as two directions summed (0.85 x 76.8,
+    DESIGN.md §7, from memory) goes beside it as `meets_per_direction_reading`,
+    unsourced until a node measurement settles which reading is the link."""
+    return dict(value=round(achieved, 2), bytes=nbytes,
+                target=f">= {TARGET_LINK_FRAC} x {STATED_LINK_PEAK_GBPS} GB/s per direction of one link "
+                       f"(SURVEY.md:361, BASELINE.md:51)",
+                meets=achieved >= TARGET_LINK_FRAC * STATED_LINK_PEAK_GBPS,
+                per_direction_reading=f">= {TARGET_LINK_FRAC} x {XGMI_LINK_PEAK_GBPS} GB/s: 153.6 read as both "
+                                      f"directions summed (DESIGN.md §7; unsourced, from memory, until a node run "
+                                      f"measures the link)",
+                meets_per_direction_reading=achieved >= TARGET_LINK_FRAC * XGMI_LINK_PEAK_GBPS)
 EXTRAS_DEADLINE_S = 150      # 64 MiB rounds + comparison engines at N > 1 (see main)
 CEILING_BYTES, CEILING_ITERS = 64 << 20, 20   # extras: the kernel engine at 64 MiB (see main)
 
 
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
+REF_SHIM = os.path.join(ROOT, "oracle", "_ref", "libshim.so")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+MPICH = "MPICH 3.3.2 shm"
+PROFILER_ENV = ("ROCP_TOOL_LIBRARIES", "ROCPROF_COUNTERS", "ROCPROFILER_LIBRARY_CTOR")
+
+
+def under_profiler() -> str | None:
+    """The profiler variable set in this process's environment, if any."""
+    return next((k for k in PROFILER_ENV if os.environ.get(k)), None)
+
+
+def reference_available() -> bool:
+    return all(os.path.exists(x) for x in (REF_BIN, REF_SHIM, MPIEXEC))
+
+
+def _cpulist(text: str) -> list[int]:
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            lo, _, hi = part.partition("-")
+            out += range(int(lo), int(hi or lo) + 1)
+    return out
+
+
+def _read(path: str) -> str:
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return ""
+
+
+def reference_cores(nranks: int, sysfs: str = "/sys/devices/system") -> dict:
+    """The host cores the reference's ranks are bound to, chosen the way its
+    launchers choose them: one NUMA node
+    (`numactl --cpunodebind=0 --membind 0`, scripts/run-1-pair.sh:62), one
+    rank per physical core in order (`--bind-to cpulist:ordered --cpu-list
+    8..17`, scripts/run-hbv3.sh:23).  Node 0 when it has nranks allowed
+    physical cores (else the node with the most); one hardware thread per
+    core (the lowest sibling); the first 8 cores of the node skipped when it
+    has 8 + nranks of them (run-hbv3's list starts at 8), else from its first.
+    Only CPUs in this process's affinity mask are used."""
+    allowed = set(os.sched_getaffinity(0))
+    nodes = {}
+    for d in sorted(glob.glob(os.path.join(sysfs, "node", "node[0-9]*"))):
+        cpus = [c for c in _cpulist(_read(os.path.join(d, "cpulist"))) if c in allowed]
+        nodes[int(os.path.basename(d)[4:])] = cpus
+    if not nodes:
+        nodes = {0: sorted(allowed)}
+    phys = {}
+    for n, cpus in nodes.items():
+        seen, cores = set(), []
+        for c in cpus:
+            sib = _cpulist(_read(os.path.join(sysfs, "cpu", f"cpu{c}", "topology", "thread_siblings_list")) or str(c))
+            first = min(sib)
+            if first not in seen and first in allowed:
+                seen.add(first)
+                cores.append(first)
+        phys[n] = cores
+    node = 0 if len(phys.get(0, [])) >= nranks else max(phys, key=lambda k: len(phys[k]))
+    cores = phys[node]
+    skip = 8 if len(cores) >= 8 + nranks else 0
+    chosen = cores[skip:skip + nranks]
+    return dict(cores=chosen, numa_node=node, node_physical_cores=len(cores), skipped_first=skip,
+                complete=len(chosen) == nranks)
+
+
+def _proc_group(pgid: int) -> list[dict]:
+    """The processes of process group pgid (from /proc): pid, ppid, name."""
+    out = []
+    for d in glob.glob("/proc/[0-9]*"):
+        st = _read(os.path.join(d, "stat"))
+        if not st:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        f = st[st.rindex(")") + 2:].split()
+        if int(f[2]) == pgid:
+            out.append(dict(pid=int(os.path.basename(d)), ppid=int(f[1]), name=name))
+    return out
+
+
+def descendants(root: int | None = None) -> list[dict]:
+    """Every live process below `root` (default: this one) in the parent
+    tree, from /proc: pid, ppid, name, state (bench.py's exit census)."""
+    root = os.getpid() if root is None else root
+    procs = {}
+    for d in glob.glob("/proc/[0-9]*"):
+        st = _read(os.path.join(d, "stat"))
+        if not st:
+            continue
+        f = st[st.rindex(")") + 2:].split()
+        procs[int(os.path.basename(d))] = dict(pid=int(os.path.basename(d)), ppid=int(f[1]), state=f[0],
+                                               name=st[st.index("(") + 1:st.rindex(")")])
+    out, frontier = [], {root}
+    while frontier:
+        kids = [p for p in procs.values() if p["ppid"] in frontier and p["pid"] != root]
+        out += kids
+        frontier = {p["pid"] for p in kids}
+    return out
+
+
+def run_reference(nranks: int, ppn: int, args: list[str], timeout: float) -> dict:
+    """One mpiexec run of the compiled reference (oracle/_ref) under MPICH
+    shared memory, its ranks bound like its launchers bind them
+    (reference_cores: `-bind-to user:<cores>`, `-membind bind:<node>`).
+    mpiexec starts in a session of its own; whatever of its process group is
+    still alive when it returns (or times out) is named in `leftover` and
+    killed, so no hydra proxy or rank outlives the leg (VERDICT r05, next 3;
+    the reference itself finalizes cleanly, mpi_perf.c:579-581).  Returns
+    rc, stderr tail, the records' (run, time_s) pairs, binding, leftover."""
+    import signal
+    pick = reference_cores(nranks)
+    tmp = tempfile.mkdtemp(prefix="cpu_base_")
+    out = dict(rc=None, stderr="", times=[], leftover=[], binding=None, cores=pick["cores"],
+               numa_node=pick["numa_node"])
+    try:
+        with open(os.path.join(tmp, "group1"), "w") as f:
+            f.write("localhost\n")
+        os.mkdir(os.path.join(tmp, "logs"))
+        env = dict(os.environ)
+        env.pop("SHIM_OUT", None)
+        tail = ["-genv", "PPN", str(ppn), "-genv", "HOST1", "localhost", "-genv", "HOST0", "127.0.0.1",
+                os.path.join(ROOT, "oracle", "ref_wrap.sh"), REF_BIN, "-f", "group1", "-n", "1", "-p", str(ppn)] + args \
+            + ["-l", "logs"]
+        forms = [["-bind-to", "user:" + ",".join(map(str, pick["cores"])), "-membind", f"bind:{pick['numa_node']}"],
+                 ["-bind-to", "user:" + ",".join(map(str, pick["cores"]))], []] if pick["complete"] else [[]]
+        for form in forms:
+            for x in glob.glob(os.path.join(tmp, "logs", "*")):
+                os.remove(x)
+            p = subprocess.Popen([MPIEXEC, "-np", str(nranks)] + form + tail, cwd=tmp, env=env,
+                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+            try:
+                _, err = p.communicate(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                _, err = p.communicate()
+                err = f"timed out after {timeout} s; " + (err or "")
+            finally:
+                left = [q for q in _proc_group(p.pid) if q["pid"] != p.pid]
+                if left:
+                    out["leftover"] += left
+                    print(f"[bench] reference leg left {left} alive: killed", file=sys.stderr)
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+            out["rc"], out["stderr"] = p.returncode, (err or "")[-400:]
+            out["binding"] = " ".join(form) if form else "none (mpiexec's default placement)"
+            if p.returncode == 0:
+                break
+        for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log")):
+            for line in open(path):
+                f = line.strip().split(",")
+                out["times"].append((int(f[10]), float(f[9]) / 1000.0))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    if not out["cores"] or out["binding"].startswith("none"):
+        out["cores"] = None
+    return out
+
+
+def _spread(rates: list[float]) -> dict:
+    return dict(min=round(min(rates), 3), median=round(statistics.median(rates), 3), max=round(max(rates), 3),
+                runs=len(rates))
+
+
+def _placement(r: dict) -> dict:
+    return dict(core_list=r["cores"], numa_node=r["numa_node"], binding=r["binding"], leftover_processes=r["leftover"])
+
+
 def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:
-    """Time the reference on the host: 2 ranks, unidirectional, B bytes."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
-    mpiexec = "/opt/conda/bin/mpiexec"
+    """Time the reference on the host: 2 ranks, unidirectional, B bytes;
+    each run's rate (runs 1..runs-1; run 0 is the reference's warm-up, never
+    recorded) and their min / median / max."""
     sample = f"-u 1 -b {nbytes} -i {iters} -r {runs}, 2 ranks, runs 1..{runs - 1} (run 0 is the reference's warm-up)"
-    if os.path.exists(ref) and os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libshim.so")) \
-            and os.path.exists(mpiexec):
-        tmp = tempfile.mkdtemp(prefix="cpu_base_")
+    if reference_available():
         try:
-            with open(os.path.join(tmp, "group1"), "w") as f:
-                f.write("localhost\n")
-            os.mkdir(os.path.join(tmp, "logs"))
-            env = dict(os.environ, PPN="1", HOST1="localhost", HOST0="127.0.0.1")
-            env.pop("SHIM_OUT", None)
-            cmd = [mpiexec, "-np", "2", "-genv", "PPN", "1", "-genv", "HOST1", "localhost", "-genv", "HOST0",
-                   "127.0.0.1", os.path.join(ROOT, "oracle", "ref_wrap.sh"), ref, "-f", "group1", "-n", "1",
-                   "-p", "1", "-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs), "-l", "logs"]
-            p = subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=300)
-            times = []
-            for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log")):
-                for line in open(path):
-                    times.append(float(line.split(",")[9]) / 1000.0)
-            if p.returncode == 0 and times:
+            r = run_reference(2, 1, ["-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs)], 300)
+            times = [t for _, t in r["times"]]
+            if r["rc"] == 0 and times:
                 t = statistics.median(times)
                 return dict(value=round(nbytes * iters / t / 1e9, 3), unit="GB/s", cores=2, kind="reference",
-                            sample="mpi_perf.c (oracle/_ref) under MPICH 3.3.2 shm, " + sample,
-                            median_run_s=t)
-            print(f"[bench] reference baseline failed rc={p.returncode}: {p.stderr[-400:]}", file=sys.stderr)
+                            sample=f"mpi_perf.c (oracle/_ref) under {MPICH}, " + sample, median_run_s=t,
+                            GBps_per_run=_spread([nbytes * iters / x / 1e9 for x in times]), **_placement(r))
+            print(f"[bench] reference baseline failed rc={r['rc']}: {r['stderr']}", file=sys.stderr)
         except Exception as e:  # noqa: BLE001
             print(f"[bench] reference baseline unavailable: {e}", file=sys.stderr)
-        finally:
-            shutil.rmtree(tmp, ignore_errors=True)
     port = os.path.join(ROOT, "oracle", "oracle_perf")
     if os.path.exists(port):
         p = subprocess.run([port, "-p", "1", "-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs)],
@@ -119,43 +294,30 @@ def cpu_baseline_pingpong(runs: int = 6) -> dict | None:
     the compiled reference's 2-rank ping-pong (mpi_perf.c:66-83, the default
     loop) under MPICH shm at 8 B (-i 20000) and 4 MiB (-i 500), SURVEY
     §8(d) cfg1's iterations, -r runs; median of runs 1..runs-1 (run 0 is the
-    reference's warm-up).  half_rtt_us_8B = time / (2 x iters); GBps_4MiB =
-    2 x B x iters / time, the reference's own formula for this loop
-    (mpi_perf.c:535-542, both directions).  ~5 s on the box, before any GPU
-    call."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
-    mpiexec = "/opt/conda/bin/mpiexec"
-    if not (os.path.exists(ref) and os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libshim.so"))
-            and os.path.exists(mpiexec)):
+    reference's warm-up), with each run's min / max beside it.
+    half_rtt_us_8B = time / (2 x iters); GBps_4MiB = 2 x B x iters / time,
+    the reference's own formula for this loop (mpi_perf.c:535-542, both
+    directions).  ~5 s on the box, before any GPU call."""
+    if not reference_available():
         return None
     out = dict(cores=2, kind="reference", loop="ping-pong (mpi_perf.c:66-83)",
-               sample=f"mpi_perf.c (oracle/_ref) under MPICH 3.3.2 shm, 2 ranks, -b 8 -i 20000 and -b 4194304 "
+               sample=f"mpi_perf.c (oracle/_ref) under {MPICH}, 2 ranks, -b 8 -i 20000 and -b 4194304 "
                       f"-i 500, -r {runs}, median of runs 1..{runs - 1}")
     for nbytes, iters, key in ((8, 20000, "half_rtt_us_8B"), (4 << 20, 500, "GBps_4MiB")):
-        tmp = tempfile.mkdtemp(prefix="cpu_base_pp_")
         try:
-            with open(os.path.join(tmp, "group1"), "w") as f:
-                f.write("localhost\n")
-            os.mkdir(os.path.join(tmp, "logs"))
-            env = dict(os.environ)
-            env.pop("SHIM_OUT", None)
-            cmd = [mpiexec, "-np", "2", "-genv", "PPN", "1", "-genv", "HOST1", "localhost", "-genv", "HOST0",
-                   "127.0.0.1", os.path.join(ROOT, "oracle", "ref_wrap.sh"), ref, "-f", "group1", "-n", "1",
-                   "-p", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs), "-l", "logs"]
-            p = subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=120)
-            times = [float(line.split(",")[9]) / 1000.0 for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log"))
-                     for line in open(path)]
-            if p.returncode != 0 or not times:
+            r = run_reference(2, 1, ["-b", str(nbytes), "-i", str(iters), "-r", str(runs)], 120)
+            times = [t for _, t in r["times"]]
+            if r["rc"] != 0 or not times:
                 out[key] = None
-                out[key + "_error"] = f"rc {p.returncode}: {p.stderr[-200:]}"
+                out[key + "_error"] = f"rc {r['rc']}: {r['stderr'][-200:]}"
                 continue
-            t = statistics.median(times)
-            out[key] = round(t / (2 * iters) * 1e6, 3) if nbytes == 8 else round(2 * nbytes * iters / t / 1e9, 3)
+            vals = [x / (2 * iters) * 1e6 if nbytes == 8 else 2 * nbytes * iters / x / 1e9 for x in times]
+            out[key] = round(statistics.median(vals), 3)
+            out[key + "_per_run"] = _spread(vals)
+            out.update(_placement(r))
         except Exception as e:  # noqa: BLE001
             out[key] = None
             out[key + "_error"] = f"{type(e).__name__}: {e}"[:200]
-        finally:
-            shutil.rmtree(tmp, ignore_errors=True)
     return out
 
 
@@ -163,50 +325,36 @@ def cpu_baseline_pairs(world: int, nbytes: int, iters: int, runs: int) -> dict |
     """The reference itself on the host beside the N >= 2 line: run-hbv3's
     layout (scripts/run-hbv3.sh:22,28: N ranks, ppn = N/2 flows, -u 1) at the
     headline's B and iterations, under MPICH shared memory — N/2 concurrent
-    pairs, each a reference process pair on the box's host cores.  A run's
-    aggregate is the pairs' bytes / the slowest sender's time (only group 1
-    writes records, mpi_perf.c:545-554; its time covers its peer's last ack),
-    the reference's implied all-pairs figure; median over runs 1..runs-1 (run 0
-    is the reference's own warm-up, never recorded).  Runs on rank 0 before
-    any GPU call."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
-    mpiexec = "/opt/conda/bin/mpiexec"
-    if not (os.path.exists(ref) and os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libshim.so"))
-            and os.path.exists(mpiexec)):
+    pairs, each a reference process pair on the box's host cores, one bound
+    core per rank (reference_cores).  A run's aggregate is the pairs' bytes /
+    the slowest sender's time (only group 1 writes records,
+    mpi_perf.c:545-554; its time covers its peer's last ack), the reference's
+    implied all-pairs figure; median over runs 1..runs-1 (run 0 is the
+    reference's own warm-up, never recorded), min / max beside it.  Runs on
+    rank 0 before any GPU call."""
+    if not reference_available():
         return None
     ppn = world // 2
-    tmp = tempfile.mkdtemp(prefix="cpu_base_pairs_")
     try:
-        with open(os.path.join(tmp, "group1"), "w") as f:
-            f.write("localhost\n")
-        os.mkdir(os.path.join(tmp, "logs"))
-        env = dict(os.environ)
-        env.pop("SHIM_OUT", None)
-        cmd = [mpiexec, "-np", str(world), "-genv", "PPN", str(ppn), "-genv", "HOST1", "localhost", "-genv", "HOST0",
-               "127.0.0.1", os.path.join(ROOT, "oracle", "ref_wrap.sh"), ref, "-f", "group1", "-n", "1",
-               "-p", str(ppn), "-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs), "-l", "logs"]
-        p = subprocess.run(cmd, cwd=tmp, env=env, capture_output=True, text=True, timeout=300)
+        r = run_reference(world, ppn, ["-u", "1", "-b", str(nbytes), "-i", str(iters), "-r", str(runs)], 300)
         per_run = {}
-        for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log")):
-            for line in open(path):
-                f = line.strip().split(",")
-                per_run.setdefault(int(f[10]), []).append(float(f[9]) / 1000.0)
-        runs_ok = [max(v) for k, v in sorted(per_run.items()) if len(v) == ppn]
-        if p.returncode != 0 or not runs_ok:
-            print(f"[bench] reference pairs baseline failed rc={p.returncode}: {p.stderr[-400:]}", file=sys.stderr)
+        for k, t in r["times"]:
+            per_run.setdefault(k, []).append(t)
+        runs_ok = [max(v) for _, v in sorted(per_run.items()) if len(v) == ppn]
+        if r["rc"] != 0 or not runs_ok:
+            print(f"[bench] reference pairs baseline failed rc={r['rc']}: {r['stderr']}", file=sys.stderr)
             return None
         t = statistics.median(runs_ok)
         return dict(value=round(ppn * nbytes * iters / t / 1e9, 3), unit="GB/s", cores=world, kind="reference",
-                    sample=f"mpi_perf.c (oracle/_ref) under MPICH 3.3.2 shm, run-hbv3 layout: {world} ranks, "
-                           f"-p {ppn} -u 1 -b {nbytes} -i {iters} -r {runs} ({ppn} concurrent pairs, one core per "
-                           f"rank); aggregate = {ppn} x B x iters / the slowest sender's time per run, median of runs "
-                           f"1..{runs - 1}",
-                    per_pair_GBps=round(nbytes * iters / t / 1e9, 3), median_run_s=t)
+                    sample=f"mpi_perf.c (oracle/_ref) under {MPICH}, run-hbv3 layout: {world} ranks, "
+                           f"-p {ppn} -u 1 -b {nbytes} -i {iters} -r {runs} ({ppn} concurrent pairs, one bound core "
+                           f"per rank); aggregate = {ppn} x B x iters / the slowest sender's time per run, median of "
+                           f"runs 1..{runs - 1}",
+                    per_pair_GBps=round(nbytes * iters / t / 1e9, 3), median_run_s=t,
+                    per_pair_GBps_per_run=_spread([nbytes * iters / x / 1e9 for x in runs_ok]), **_placement(r))
     except Exception as e:  # noqa: BLE001
         print(f"[bench] reference pairs baseline unavailable: {e}", file=sys.stderr)
         return None
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def traffic_from_profile(workload: str) -> dict | None:
@@ -220,18 +368,15 @@ def traffic_from_profile(workload: str) -> dict | None:
         return json.load(f)
 
 
-PROFILER_ENV = ("ROCP_TOOL_LIBRARIES", "ROCPROF_COUNTERS", "ROCPROFILER_LIBRARY_CTOR")
-
-
 def counters_skip_reason(args) -> str | None:
     """None when the in-process counters may run; else why not.  A process
     that rocprofv3 already profiles has its own rocprofiler tool (and
     dispatch counting serialises kernels): no second one is added."""
     if args.no_counters:
         return "--no-counters"
-    for k in PROFILER_ENV:
-        if os.environ.get(k):
-            return f"not sampled in-process: the process runs under a profiler ({k} set)"
+    k = under_profiler()
+    if k:
+        return f"not sampled in-process: the process runs under a profiler ({k} set)"
     return None
 
 
@@ -783,10 +928,16 @@ PEER_CONTROL_BYTES, PEER_CONTROL_ITERS, PEER_CONTROL_BAND = 16 << 20, 8, (0.95, 
 
 
 def link_formula_bytes(v: dict) -> dict:
-    """bytes each candidate link formula reads from one set of counter values"""
-    return dict(subtraction=(v["TCC_EA0_WRREQ_sum"] - v["TCC_EA0_WRREQ_DRAM_sum"]) * 64,
-                gmi=v["TCC_EA0_WRREQ_WRITE_GMI_32B_sum"] * 32,
-                io=v["TCC_EA0_WRREQ_WRITE_IO_32B_sum"] * 32)
+    """bytes each candidate link formula reads from one set of counter values
+    (a formula whose counters are missing is left out)"""
+    out = {}
+    if "TCC_EA0_WRREQ_sum" in v and "TCC_EA0_WRREQ_DRAM_sum" in v:
+        out["subtraction"] = (v["TCC_EA0_WRREQ_sum"] - v["TCC_EA0_WRREQ_DRAM_sum"]) * 64
+    if "TCC_EA0_WRREQ_WRITE_GMI_32B_sum" in v:
+        out["gmi"] = v["TCC_EA0_WRREQ_WRITE_GMI_32B_sum"] * 32
+    if "TCC_EA0_WRREQ_WRITE_IO_32B_sum" in v:
+        out["io"] = v["TCC_EA0_WRREQ_WRITE_IO_32B_sum"] * 32
+    return out
 
 
 def peer_link_control(mpx, prof, bus: str, dev: int, peer_dev: int) -> dict:
@@ -835,24 +986,33 @@ def peer_link_control(mpx, prof, bus: str, dev: int, peer_dev: int) -> dict:
                 t.join()
 
         for name, work in (("copy", copy), ("push", push)):
+            # rx1 poisoned before each phase and checked right after it, so
+            # the copy's check sees the copy's bytes, not the push's
+            c.fill(rx1, B, mpx.FILL_BYTE, 0)
             work()
+            out[f"{name}_checked"] = c.checksum(rx1, B) == c.checksum(tx0, B)
             vals = {}
             for names in (LINK_COUNTERS, FABRIC_COUNTERS):
-                with prof.Pass(bus, list(names)) as p:
-                    work()
-                vals.update(zip(names, p.values))
+                try:
+                    with prof.Pass(bus, list(names)) as p:
+                        work()
+                    vals.update(zip(names, p.values))
+                except Exception as e:  # noqa: BLE001
+                    if names is LINK_COUNTERS:
+                        raise
+                    out[f"{name}_fabric_error"] = f"{type(e).__name__}: {e}"[:160]   # optional set
             fb = link_formula_bytes(vals)
+            dram32 = vals.get("TCC_EA0_WRREQ_WRITE_DRAM_32B_sum")
             out[name] = dict({f"{k}_over_bytes": round(v / (B * IT), 5) for k, v in fb.items()},
-                             dram_over_bytes=round(vals["TCC_EA0_WRREQ_WRITE_DRAM_32B_sum"] * 32 / (B * IT), 5),
+                             dram_over_bytes=None if dram32 is None else round(dram32 * 32 / (B * IT), 5),
                              raw=vals)
-        out["copy_checked"] = c.checksum(rx1, B) == c.checksum(tx0, B)
         if errs:
             out["push_errors"] = errs
     finally:
         c.close()
     lo, hi = PEER_CONTROL_BAND
-    out["validated_formula"] = next((f for f in LINK_FORMULAS
-                                     if out["copy_checked"] and lo <= out["copy"][f"{f}_over_bytes"] <= hi), None)
+    out["validated_formula"] = next((f for f in LINK_FORMULAS if out["copy_checked"] and f"{f}_over_bytes" in
+                                     out["copy"] and lo <= out["copy"][f"{f}_over_bytes"] <= hi), None)
     return out
 
 
@@ -893,7 +1053,11 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
                 vals["reads_reset"] = p.reads_reset
             except Exception as e:  # noqa: BLE001
                 notes.append(f"rank {rank}: {type(e).__name__}: {e}"[:200])
-    mine = [1.0 if (sampler and all(k in vals for k in ALL_COUNTERS)) else 0.0]
+    # sampled = the link and read sets were read; the fabric set is optional
+    # (one GMI/IO counter unavailable nulls only its own figures)
+    required = LINK_COUNTERS + READ_COUNTERS
+    mine = [1.0 if (sampler and all(k in vals for k in required)) else 0.0,
+            1.0 if (sampler and all(k in vals for k in FABRIC_COUNTERS)) else 0.0]
     mine += [float(vals.get(k, 0.0)) for k in ALL_COUNTERS] + [g1_s, float(g1_n)]
     every = [torch.zeros(len(mine), dtype=torch.float64) for _ in range(world)]
     dist.all_gather(every, torch.tensor(mine, dtype=torch.float64))
@@ -904,7 +1068,8 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
     got = [e for e in every if float(e[0]) == 1.0]
     if len(got) != want:
         return {"error": "; ".join(notes) or "not every GPU was sampled", "samplers": want, "sampled": len(got)}
-    tot = [sum(float(e[1 + k]) for e in got) for k in range(len(ALL_COUNTERS))]
+    tot = [sum(float(e[2 + k]) for e in got) for k in range(len(ALL_COUNTERS))]
+    fabric = all(float(e[1]) == 1.0 for e in got)
     wr, w64, dram, rd, rd_dram, gmi32, io32, dram32 = tot
     launches = (world // 2) * len(rounds)
     alg = nbytes * iters * launches
@@ -912,6 +1077,12 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
     g1_avg = sum(float(e[-2]) for e in every) / max(sum(float(e[-1]) for e in every), 1.0)
     link = (wr - dram) * 64
     formulas = link_formula_bytes(dict(zip(ALL_COUNTERS, tot)))
+    if not fabric:
+        formulas = {k: v for k, v in formulas.items() if k == "subtraction"}
+        notes.append("fabric counters (GMI / IO 32-B writes) not read on every sampler: their figures are null")
+
+    def fab(v, digits):
+        return round(v, digits) if fabric else None
     out = dict(
         source="in-process rocprofiler-sdk device counting service (mpi-perf_amd/lib/libmpxprof.so), one pass per "
                "counter set over an untimed re-run of every round (the timed steps' loop, width and hint), one "
@@ -924,8 +1095,9 @@ def link_counters(mpx, prof, torch, dist, c, rounds, rank, world, tx, rx, nbytes
         link_over_algorithmic=round(link / alg, 5), local_dram_over_algorithmic=round(dram * 64 / alg, 5),
         write_requests_64B_fraction=round(w64 / wr, 5) if wr else None,
         read_requests_per_launch=round(rd / launches, 1), read_dram_requests_per_launch=round(rd_dram / launches, 1),
-        gmi_write_bytes_per_launch=round(gmi32 * 32 / launches, 1), io_write_bytes_per_launch=round(io32 * 32 / launches, 1),
-        gmi_over_algorithmic=round(gmi32 * 32 / alg, 5), io_over_algorithmic=round(io32 * 32 / alg, 5),
+        gmi_write_bytes_per_launch=fab(gmi32 * 32 / launches, 1), io_write_bytes_per_launch=fab(io32 * 32 / launches, 1),
+        gmi_over_algorithmic=fab(gmi32 * 32 / alg, 5), io_over_algorithmic=fab(io32 * 32 / alg, 5),
+        fabric_counters_read=fabric,
         g1_avg_launch_us=round(g1_avg * 1e6, 2),
         achieved_link_GBps_per_pair=round(link / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
         achieved_local_dram_GBps_per_pair=round(dram * 64 / launches / g1_avg / 1e9, 2) if g1_avg > 0 else None,
@@ -970,7 +1142,7 @@ def link_traffic(cnt: dict) -> dict:
                     traffic_source=src, traffic_check="not applicable: ranks share a GPU (local pushes, ~0 expected)")
     pc = cnt.get("peer_control") or {}
     f = pc.get("validated_formula")
-    if f:
+    if f and f in cnt["link_formula_over_algorithmic"]:
         # a formula validated on THIS node by known bytes across a link (an
         # independent writer): it measures the pushes, whatever they read
         fr = cnt["link_formula_over_algorithmic"][f]
@@ -1420,13 +1592,26 @@ def main() -> None:
     # the reference in run-hbv3's layout at the headline's B and iterations
     # (the other ranks wait in the process-group init meanwhile)
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    prof_var = under_profiler()
+    if rank == 0 and not args.no_cpu_baseline and prof_var:
+        # Under rocprofv3 the profiler's preload and ROCP_* variables would
+        # pass through mpiexec to oracle/ref_wrap.sh, whose `exec` would then
+        # follow a GPU initialisation (with --pmc the preload initialises the
+        # GPU): the reference legs are not started
+        cpu = dict(value=None, unit="GB/s", cores=0, kind="reference",
+                   sample=f"not run: this process runs under a profiler ({prof_var} set)")
+    elif rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(nbytes, 16, 6) if one else cpu_baseline_pairs(world, nbytes, iters, 6)
         # BASELINE config 1 itself (the reference's 2-rank ping-pong at 8 B
         # and 4 MiB) beside every line, whatever the workload
         pp = cpu_baseline_pingpong()
         if cpu is not None and pp is not None:
             cpu["config1_pingpong"] = pp
+        # no process of the reference legs may outlive them (run_reference
+        # kills their groups): the census says so before any GPU call
+        cpu_left = descendants()
+        if cpu is not None:
+            cpu["processes_left_by_baseline"] = cpu_left
 
     import torch
     import mpx
@@ -1566,7 +1751,9 @@ def main() -> None:
         achieved = res["per_pair_GBps"]
         roof = dict(bound="xgmi", achieved=round(achieved, 2), peak=XGMI_LINK_PEAK_GBPS, unit="GB/s",
                     frac=round(achieved / XGMI_LINK_PEAK_GBPS, 4), traffic=None,
-                    peak_note="one direction of one xGMI link (153.6 GB/s bidirectional per link)",
+                    peak_note=("one direction of one xGMI link under the per-direction reading (153.6 GB/s as both "
+                               "directions summed, DESIGN.md §7, unsourced); frac_of_bidirectional_link is against "
+                               "153.6, the per-direction figure SURVEY.md:361 states and extras.targets judges by"),
                     frac_of_bidirectional_link=round(achieved / XGMI_LINK_PEAK_BIDIR_GBPS, 4),
                     kernel="k_xfer (G1 side)" if engine_used == "kernel" else engine_used,
                     avg_launch_us=round(res["per_launch_s"] * 1e6, 2), algorithmic_bytes_per_launch=nbytes * iters,
@@ -1637,11 +1824,7 @@ def main() -> None:
         # each north_star target beside the number it judges (extras.targets)
         tg = {}
         if nbytes >= (4 << 20):
-            tg["per_pair_unidir_GBps"] = dict(
-                value=round(achieved, 2), bytes=nbytes,
-                target=f">= {TARGET_LINK_FRAC} x {XGMI_LINK_PEAK_GBPS} GB/s (one direction of one link)",
-                meets=achieved >= TARGET_LINK_FRAC * XGMI_LINK_PEAK_GBPS,
-                meets_vs_bidirectional_153_6=achieved >= TARGET_LINK_FRAC * XGMI_LINK_PEAK_BIDIR_GBPS)
+            tg["per_pair_unidir_GBps"] = link_target(achieved, nbytes)
         if extras.get("pingpong_8B_half_rtt_us") is not None:
             v = extras["pingpong_8B_half_rtt_us"]
             tg["pingpong_8B_half_rtt_us"] = dict(value=v, target=f"< {TARGET_HALF_RTT_US} us",
@@ -1655,7 +1838,7 @@ def main() -> None:
         if os.environ.get("MPX_BENCH_ONE_GPU"):
             # every rank on GPU 0: loopback pairs, no xGMI link was measured
             for t in tg.values():
-                for k in ("meets", "meets_vs_bidirectional_153_6"):
+                for k in ("meets", "meets_per_direction_reading"):
                     if k in t:
                         t[k] = None
             tg["note"] = "MPX_BENCH_ONE_GPU rehearsal: loopback pairs on one GPU, not an xGMI measurement"
@@ -1736,6 +1919,10 @@ def main() -> None:
             done.set()
         dog.cancel()
     if rank == 0:
+        # exit census: this process's live descendants
+        # as the line goes out (none expected: every reference leg's process
+        # group was killed, and libmpx starts no process)
+        extras["processes_at_line"] = descendants()
         emit(out_fd, line)
     if dist is not None:
         dist.barrier()
@@ -1756,6 +1943,8 @@ def main() -> None:
     sys.stdout.flush()
     sys.stderr.flush()
     mpx.shutdown()
+    left = descendants()
+    print(f"[bench] rank {rank}: processes left at exit: {left if left else 'none'}", file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -196,6 +196,10 @@ int mpx_finalize(mpx_ctx *ctx);
    the runtime) if the stream fence did not complete in 10 s.  May be called
    mid-process: a later context creates new rank streams. */
 int mpx_shutdown(void);
+/* Diagnostic: HIP events this library holds right now, across every context
+   (each is owned by an RAII holder and destroyed on every return path:
+   the tests' leak check around a failing mpx_copy, MPX_TEST=fail_copy). */
+int mpx_live_events(int *count);
 
 /* ---- buffers (allocate_tx_rx_buffers, mpi_perf.c:240-252) ---------------- */
 /* posix_memalign(4096) analogue: device memory on `dev`, 4 KiB aligned.  The

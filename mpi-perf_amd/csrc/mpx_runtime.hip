@@ -159,6 +159,49 @@ struct DeviceGuard {
     }
 };
 
+// Owns one HIP event: destroyed when its holder goes (scope exit on any
+// path, an early HIPCK return included, or the owning Rank's reset), so no
+// error path can leak it.  live_events() counts the events alive in the
+// process (mpx_live_events: the tests' leak check).
+std::atomic<int>& live_events() {
+    static std::atomic<int> n{0};
+    return n;
+}
+
+class Event {
+  public:
+    Event() = default;
+    Event(const Event&) = delete;
+    Event& operator=(const Event&) = delete;
+    Event(Event&& o) noexcept : e_(o.e_) { o.e_ = nullptr; }
+    Event& operator=(Event&& o) noexcept {
+        if (this != &o) {
+            reset();
+            e_ = o.e_;
+            o.e_ = nullptr;
+        }
+        return *this;
+    }
+    ~Event() { reset(); }
+    hipError_t create() {
+        reset();
+        const hipError_t e = hipEventCreate(&e_);
+        if (e == hipSuccess) live_events().fetch_add(1);
+        else e_ = nullptr;
+        return e;
+    }
+    void reset() {
+        if (!e_) return;
+        (void)hipEventDestroy(e_);
+        e_ = nullptr;
+        live_events().fetch_sub(1);
+    }
+    operator hipEvent_t() const { return e_; }
+
+  private:
+    hipEvent_t e_ = nullptr;
+};
+
 enum MailboxKind { kMbUncached = 0, kMbFine = 1, kMbCoarse = 2 };
 
 // (mode, group, peer rank, bytes, timeout ticks, iterations) of a captured
@@ -180,7 +223,7 @@ struct Rank {
     Mailbox* mb = nullptr;         // usable from this process
     int mb_kind = kMbUncached;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    Event ev0, ev1;                // start / end of the rank's last call (RAII)
     u64 token = 0;                 // kernel-engine calls made: Status.done of the last one
     mpx_phases phases{};           // the last kernel-engine call (mpx_last_phases)
     struct KernelCall* armed = nullptr;   // the call mpx_xfer_arm launched, not started yet
@@ -421,6 +464,8 @@ u64 nb_waited(int iters) {
 //   fail_launch=r   rank r's kernel-engine calls fail before their kernel is
 //                   enqueued (after prepare_call took their numbers): the
 //                   rollback test of unprepare_call
+//   fail_copy       mpx_copy fails after its events are created and the start
+//                   one is recorded: the event-leak test (mpx_live_events)
 // Whether the variable exists is read ONCE per process: a process that
 // starts without it (bench.py, mpx_perf) never looks again, and none of the
 // knobs can reach it.  The tests set it (empty) before their first call
@@ -431,6 +476,7 @@ struct TestKnobs {
     long long lag_us = 0;
     bool no_posted = false, no_pull_wait = false;
     int fail_launch = -1;
+    bool fail_copy = false;
 };
 TestKnobs test_knobs() {
     static const bool gate = getenv("MPX_TEST") != nullptr;
@@ -450,6 +496,7 @@ TestKnobs test_knobs() {
         } else if (item == "no_posted") k.no_posted = true;
         else if (item == "no_pull_wait") k.no_pull_wait = true;
         else if (!item.compare(0, 12, "fail_launch=")) k.fail_launch = atoi(item.c_str() + 12);
+        else if (item == "fail_copy") k.fail_copy = true;
         pos = end + 1;
     }
     return k;
@@ -591,13 +638,13 @@ bool callback_fence(const std::vector<std::pair<int, hipStream_t>>& ss) {
     return done && handed_off;
 }
 
-// A rank stream goes back to the pool; it is never destroyed while the
-// process runs.  Round 2's opt-in destroy per finalize (MPX_STREAM_POOL=0)
-// is gone: with callback_fence in place of its 50 ms wait the engine tests
-// still stalled inside a later mpx_finalize (profiles/r03_pytest_nopool.log),
-// as they did after a device-wide synchronize (r02_stream_destroy_devsync.txt)
-// — destroying a CU-masked stream mid-process is unsafe on this runtime
-// whatever ordering precedes it, so the pool is the design, not a default.
+// A rank stream goes back to the pool at finalize; later contexts reuse it
+// (a CU-masked queue costs a KFD queue creation).  Pooled streams are
+// destroyed only by mpx_shutdown, once no context is alive — which may be
+// mid-process (mpx.h; tests/test_gpu_teardown.py): callback_fence and its
+// event_thread_barrier order that destroy after every completion handler's
+// release (round 5's root cause of the stalls rounds 2-4 saw, when each
+// finalize destroyed its streams, profiles/r03_pytest_nopool.log).
 void release_rank_stream(int dev, hipStream_t s) {
     std::lock_guard<std::mutex> lk(pool().mu);
     pool().idle[dev].push_back(s);
@@ -1614,8 +1661,8 @@ int mpx_finalize(mpx_ctx* ctx) {
         Rank& rk = ctx->r[i];
         if (!rk.local) continue;
         DeviceGuard g(rk.dev);
-        if (rk.ev0) (void)hipEventDestroy(rk.ev0);
-        if (rk.ev1) (void)hipEventDestroy(rk.ev1);
+        rk.ev0.reset();
+        rk.ev1.reset();
         if (rk.stream) release_rank_stream(rk.dev, rk.stream);
     }
     if (fenced) {   // else left to the runtime: a destroy could be the events thread's last release
@@ -1746,9 +1793,9 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
     TRY(util_stream(ctx, dev, &s));
     std::lock_guard<std::mutex> ul(ctx->util_mu);
     DeviceGuard g(dev);
-    hipEvent_t e0, e1;
-    HIPCK(hipEventCreate(&e0));
-    HIPCK(hipEventCreate(&e1));
+    Event e0, e1;   // destroyed on every return below
+    HIPCK(e0.create());
+    HIPCK(e1.create());
     int grid = 0;
     // All iterations in one launch where a launch per copy is dispatch-bound:
     // k_copy_pipe above 512 KiB to 16 MiB, k_copy_steps up to 512 KiB; one
@@ -1767,6 +1814,7 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
         if (one) HIPCK(hipMemsetAsync(bar, 0, 17 * 16 * sizeof(u64), s));   // top + 8 group counters + 8 release words
         t0 = now_s();
         HIPCK(hipEventRecord(e0, s));
+        if (test_knobs().fail_copy) return fail(MPX_ERR_HIP, "copy failed after its start event (MPX_TEST fail_copy)");
         if (one && pipe) {
             const hipError_t e = launch_copy_pipe(dst, src, n, iters, bar, s, &grid, cc.upl, cc.hier);
             if (e == hipErrorInvalidValue) {
@@ -1797,8 +1845,6 @@ int mpx_copy(mpx_ctx* ctx, int dev, void* dst, const void* src, size_t n, int it
         one = false;
     }
     t->wall_s = now_s() - t0;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     t->device_s = ms * 1e-3;
     t->bytes = (uint64_t)n * (uint64_t)iters;
     t->launches = !n ? 0 : one ? 1 : iters;
@@ -1816,8 +1862,8 @@ int attach_resources(Rank& rk) {
     TRY(alloc_mailbox(rk));
     TRY(create_rank_stream(rk.dev, &rk.stream));
     HIPCK(hipMemsetAsync(rk.mb, 0, sizeof(Mailbox), rk.stream));
-    HIPCK(hipEventCreate(&rk.ev0));
-    HIPCK(hipEventCreate(&rk.ev1));
+    HIPCK(rk.ev0.create());
+    HIPCK(rk.ev1.create());
     HIPCK(hipHostMalloc(reinterpret_cast<void**>(&rk.status), sizeof(Status), hipHostMallocCoherent | hipHostMallocMapped));
     memset(rk.status, 0, sizeof(Status));
     HIPCK(hipMalloc(&rk.scratch, kScratchWords * sizeof(u64)));
@@ -1838,8 +1884,8 @@ void release_rank(Rank& rk) {
     if (rk.csum) (void)hipFree(rk.csum);
     for (void* q : rk.retired) (void)hipFree(q);
     if (rk.status) (void)hipHostFree(rk.status);
-    if (rk.ev0) (void)hipEventDestroy(rk.ev0);
-    if (rk.ev1) (void)hipEventDestroy(rk.ev1);
+    rk.ev0.reset();
+    rk.ev1.reset();
     if (rk.stream) release_rank_stream(rk.dev, rk.stream);
     (void)hipGetLastError();
     rk = Rank{};
@@ -1898,7 +1944,7 @@ int mpx_rank_attach(mpx_ctx* ctx, int rank, int dev, void* tx, void* rx, size_t 
         return st;
     }
     if (ctx->import_dev < 0) ctx->import_dev = dev;
-    ctx->r[rank] = rk;
+    ctx->r[rank] = std::move(rk);
     return MPX_OK;
 }
 
@@ -1969,7 +2015,7 @@ int mpx_rank_import(mpx_ctx* ctx, int rank, const void* desc) {
         ctx->ipc_opened.push_back(p);
         rk.ring = static_cast<unsigned char*>(p);
     }
-    ctx->r[rank] = rk;
+    ctx->r[rank] = std::move(rk);
     return MPX_OK;
 }
 
@@ -2219,15 +2265,34 @@ int mpx_shutdown(void) {
     if (p.all.empty()) return MPX_OK;
     if (!callback_fence(p.all))
         return fail(MPX_ERR_TIMEOUT, "stream fence did not complete in 10 s: streams left to the runtime");
+    // every stream is destroyed and forgotten, whatever one destroy returns
+    // (a stream left in the pool after a failed destroy could be handed out
+    // again, or destroyed twice by a second shutdown); the first error is
+    // the result, reported after the caller's device is restored
     int prev = -1;
     (void)hipGetDevice(&prev);
+    hipError_t first = hipSuccess;
+    int first_dev = -1;
     for (auto& ds : p.all) {
         (void)hipSetDevice(ds.first);
-        HIPCK(hipStreamDestroy(ds.second));
+        const hipError_t e = hipStreamDestroy(ds.second);
+        if (e != hipSuccess && first == hipSuccess) {
+            first = e;
+            first_dev = ds.first;
+        }
     }
+    (void)hipGetLastError();
     if (prev >= 0) (void)hipSetDevice(prev);
     p.all.clear();
     p.idle.clear();
+    if (first != hipSuccess)
+        return fail(MPX_ERR_HIP, "hipStreamDestroy on device %d: %s", first_dev, hipGetErrorString(first));
+    return MPX_OK;
+}
+
+int mpx_live_events(int* count) {
+    if (!count) return fail(MPX_ERR_INVALID, "NULL argument");
+    *count = live_events().load();
     return MPX_OK;
 }
 

@@ -95,6 +95,7 @@ _SIGS = {
     "mpx_init": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "mpx_finalize": (C.c_int, [C.c_void_p]),
     "mpx_shutdown": (C.c_int, []),
+    "mpx_live_events": (C.c_int, [C.POINTER(C.c_int)]),
     "mpx_alloc": (C.c_int, [C.c_void_p, C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]),
     "mpx_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mpx_fill": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_int, C.c_uint64]),
@@ -172,6 +173,13 @@ def link_info(dev_a: int, dev_b: int) -> dict:
 def shutdown() -> None:
     """mpx_shutdown: destroy the pooled rank streams (no context alive)."""
     check(lib().mpx_shutdown(), "mpx_shutdown")
+
+
+def live_events() -> int:
+    """mpx_live_events: HIP events libmpx holds right now (leak check)."""
+    n = C.c_int(0)
+    check(lib().mpx_live_events(C.byref(n)), "mpx_live_events")
+    return n.value
 
 
 def bus_id(dev: int) -> str:

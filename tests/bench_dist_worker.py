@@ -37,7 +37,7 @@ class FakeError(RuntimeError):
 class FakeMpx:
     """Mirror of the mpx binding's surface that bench.pairs_bench uses."""
     MODE_PINGPONG, MODE_NONBLOCKING, MODE_UNIDIR = 0, 1, 2
-    FILL_SPLITMIX = 1
+    FILL_BYTE, FILL_SPLITMIX = 0, 1
     PATTERN_SEED = 0x6D70695F70657266
     log = []
 
@@ -180,6 +180,8 @@ class FakeProf:
 
         def __exit__(self, *exc):
             FakeMpx.log.append(["pass_end", self.names])
+            if scenario == "fabric_missing" and "TCC_EA0_WRREQ_WRITE_GMI_32B_sum" in self.names:
+                raise RuntimeError("counter TCC_EA0_WRREQ_WRITE_GMI_32B_sum not available on this agent")
             self.values = [FakeProf.COUNTS[n] for n in self.names]
             return False
 
@@ -223,9 +225,10 @@ if __name__ == "__main__":
         else:
             # one_gpu: only rank 0 registers the tool (bench.main's one-GPU
             # rehearsal); counters_missing: sampling rank 1 has none
-            prof = FakeProf if (scenario in ("counters", "counters_validated") or (scenario == "one_gpu" and rank == 0)
+            prof = FakeProf if (scenario in ("counters", "counters_validated", "fabric_missing")
+                                or (scenario == "one_gpu" and rank == 0)
                                 or (scenario == "counters_missing" and rank != 1)) else None
-            count = scenario in ("counters", "counters_validated", "one_gpu", "counters_missing")
+            count = scenario in ("counters", "counters_validated", "one_gpu", "counters_missing", "fabric_missing")
             # the per-round barriers spin in shared memory, as in bench.main (world 2 and 4 here)
             d, spin = bench.spin_barrier_dist(dist, rank, world) if scenario == "ok" else (dist, None)
             out["spin"] = spin is not None

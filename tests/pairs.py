@@ -17,15 +17,19 @@ import threading
 
 import mpx
 
-# MPX_MULTI_REHEARSE=1: run the multi-GPU tests' code on one GPU (every rank
-# on GPU 0) to shake out the tests themselves; see tests/test_gpu_multi.py
-REHEARSE = bool(os.environ.get("MPX_MULTI_REHEARSE"))
+def rehearsing() -> bool:
+    """MPX_MULTI_REHEARSE=1: run the multi-GPU tests' code on one GPU (every
+    rank on GPU 0) to shake out the tests themselves.  Read per call: on a
+    one-GPU box tests/test_gpu_multi.py sets it per test (a fixture), so the
+    driver's `pytest -m gpu` runs that rehearsal; subprocess workers inherit
+    it through the environment."""
+    return bool(os.environ.get("MPX_MULTI_REHEARSE"))
 
 
 def cross_gpu_devs(nranks: int) -> list[int] | None:
     """rank r on GPU r, or None when fewer than nranks GPUs are visible
     (rehearsal: every rank on GPU 0)"""
-    if REHEARSE:
+    if rehearsing():
         return [0] * nranks
     return list(range(nranks)) if mpx.device_count() >= nranks else None
 

@@ -377,3 +377,39 @@ def test_cpu_baseline_beside_the_pairs_line(world):
     assert cb and cb["kind"] == "reference" and cb["cores"] == world and cb["unit"] == "GB/s"
     assert cb["value"] > 0 and cb["per_pair_GBps"] == pytest.approx(cb["value"] / (world // 2), rel=1e-2)
     assert f"{world} ranks, -p {world // 2} -u 1 -b {1 << 20} -i 40 -r 3" in cb["sample"]
+
+
+def test_link_target_primary_verdict_follows_the_stated_bar():
+    """extras.targets.per_pair_unidir_GBps: `meets` is
+    judged against the stated bar, 0.85 x 153.6 GB/s per direction
+    (SURVEY.md:361, BASELINE.md:51); the unsourced per-direction reading
+    (0.85 x 76.8) goes beside it as meets_per_direction_reading."""
+    assert bench.STATED_LINK_PEAK_GBPS == 153.6 and bench.XGMI_LINK_PEAK_GBPS == 76.8
+    for gbps, primary, reading in ((131.0, True, True), (130.0, False, True), (66.0, False, True),
+                                   (65.0, False, False)):
+        t = bench.link_target(gbps, 4 << 20)
+        assert t["meets"] is primary and t["meets_per_direction_reading"] is reading, (gbps, t)
+        assert "153.6 GB/s per direction" in t["target"] and "SURVEY.md:361" in t["target"]
+        assert "76.8" in t["per_direction_reading"] and "unsourced" in t["per_direction_reading"]
+        assert "meets_vs_bidirectional_153_6" not in t
+
+
+def test_fabric_counters_are_optional(tmp_path):
+    """the GMI / IO / DRAM 32-B write counters are an optional
+    set.  When their pass fails on a sampler, the link and read figures still
+    stand (no error), the fabric figures are null, the 'gmi' / 'io' formulas
+    are left out, and the peer control still reports the subtraction."""
+    res = run(2, "fabric_missing", tmp_path)
+    for d in res:
+        cnt = d["res"]["counters"]
+        assert "error" not in cnt, cnt
+        assert cnt["fabric_counters_read"] is False and cnt["gmi_write_bytes_per_launch"] is None
+        assert cnt["link_bytes_per_launch"] == round(2 * 990 * 64 / 1, 1)
+        assert set(cnt["link_formula_bytes_per_launch"]) == {"subtraction"}
+        assert any("fabric counters" in n for n in cnt["notes"])
+        if d["rank"] == 0:
+            pc = cnt["peer_control"]
+            assert "subtraction_over_bytes" in pc["copy"] and "gmi_over_bytes" not in pc["copy"], pc
+            assert "copy_fabric_error" in pc and pc["copy_checked"] is True and pc["push_checked"] is True
+        roof = bench.link_traffic(cnt)
+        assert roof["traffic_check"] == "failed" and "None" in roof["traffic_reason"]

@@ -68,3 +68,60 @@ def test_config1_pingpong_baseline_shape():
     assert pp is not None, "oracle/_ref not built (python -c 'import __graft_entry__ as g; g.build()')"
     assert pp["cores"] == 2 and pp["kind"] == "reference" and pp["loop"].startswith("ping-pong")
     assert 0 < pp["half_rtt_us_8B"] < 100 and 0 < pp["GBps_4MiB"] < 1000, pp
+
+
+def test_config1_pingpong_binds_like_the_launchers_and_leaves_no_process():
+    """the reference's ranks run bound, one physical
+    core each on one NUMA node (`-bind-to user:<cores> -membind bind:<node>`,
+    as scripts/run-1-pair.sh:62 and run-hbv3.sh:23 bind them), each run's
+    spread is in the line, and nothing of mpiexec's process group outlives
+    the leg (no descendant of this process, none named as left over)."""
+    pp = bench.cpu_baseline_pingpong()
+    assert pp is not None
+    assert pp["binding"].startswith("-bind-to user:") and "-membind bind:" in pp["binding"], pp["binding"]
+    assert len(pp["core_list"]) == 2 and len(set(pp["core_list"])) == 2
+    assert pp["leftover_processes"] == [] and bench.descendants() == []
+    for key in ("half_rtt_us_8B", "GBps_4MiB"):
+        s = pp[key + "_per_run"]
+        assert s["runs"] == 5 and s["min"] <= pp[key] == s["median"] <= s["max"], (key, s)
+
+
+def _fake_sysfs(root, nodes, siblings):
+    for n, cpus in nodes.items():
+        d = root / "node" / f"node{n}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cpus + "\n")
+    for c, sib in siblings.items():
+        d = root / "cpu" / f"cpu{c}" / "topology"
+        d.mkdir(parents=True)
+        (d / "thread_siblings_list").write_text(sib + "\n")
+
+
+def test_reference_cores_one_node_one_thread_per_core(tmp_path, monkeypatch):
+    """Two nodes of 12 cores with SMT siblings 24..47: node 0's physical
+    cores, siblings dropped, the first 8 skipped when the node has 8 + n
+    (run-hbv3.sh:23's `--cpu-list 8..17`), else from its first core; only
+    CPUs in the affinity mask count."""
+    nodes = {0: "0-11,24-35", 1: "12-23,36-47"}
+    sib = {c: f"{c % 24},{c % 24 + 24}" for c in range(48)}
+    _fake_sysfs(tmp_path, nodes, sib)
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(48)))
+    r = bench.reference_cores(2, str(tmp_path))
+    assert r["numa_node"] == 0 and r["cores"] == [8, 9] and r["complete"], r
+    r = bench.reference_cores(8, str(tmp_path))
+    assert r["cores"] == list(range(8)) and r["skipped_first"] == 0, r
+    # node 0 outside the mask: the node with the most allowed physical cores
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(12, 24)) | set(range(36, 48)))
+    r = bench.reference_cores(4, str(tmp_path))
+    assert r["numa_node"] == 1 and r["cores"] == [20, 21, 22, 23] and r["complete"], r   # 12 >= 8 + 4: skip 8
+
+
+def test_reference_legs_not_started_under_a_profiler(monkeypatch):
+    """under rocprofv3 the reference's mpiexec chain would
+    exec ref_wrap.sh after the profiler's preload initialised the GPU; bench
+    names the profiler variable and starts no reference leg."""
+    monkeypatch.setenv("ROCP_TOOL_LIBRARIES", "/x/librocprofiler-sdk-tool.so")
+    assert bench.under_profiler() == "ROCP_TOOL_LIBRARIES"
+    src = open(bench.__file__).read()
+    main = src[src.index("def main()"):]
+    assert main.index("prof_var = under_profiler()") < main.index("cpu_baseline(nbytes")

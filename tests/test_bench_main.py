@@ -47,6 +47,12 @@ def test_one_json_line_with_the_contract_keys():
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["scaling"] == "weak" and d["unit"] == "GB/s"
     assert d["config"]["workload"] == "all_pairs_rounds_unidir" and d["config"]["engine"] == "kernel"
     assert d["roofline"]["bound"] == "xgmi" and d["roofline"]["peak"] == 76.8
+    assert "frac_of_bidirectional_link" in d["roofline"]
+    # the target's primary verdict is against the stated 153.6 GB/s per
+    # direction (SURVEY.md:361); the per-direction reading beside it
+    tg = d["extras"]["targets"]["per_pair_unidir_GBps"]
+    assert tg["meets"] == (tg["value"] >= 0.85 * 153.6) and "SURVEY.md:361" in tg["target"]
+    assert tg["meets_per_direction_reading"] == (tg["value"] >= 0.85 * 76.8)
     assert isinstance(d["extras"]["sdma_aggregate_GBps"], float)
     # the pulled forms of the kernel and SDMA engines over the same rounds
     assert isinstance(d["extras"]["kernel_pull_aggregate_GBps"], float), d["extras"]

@@ -14,12 +14,17 @@ configuration each covers:
 Every payload is checksummed on the receiving device; receive accounting is
 compared with the compiled reference's golden runs where one exists.
 
-MPX_MULTI_REHEARSE=1 (with MPX_LL_MAX=8192, the cross-GPU LL threshold) runs
-this module on ONE GPU, every rank on GPU 0 and N = MPX_MULTI_REHEARSE_N
-(default 4) ranks where a test uses the whole node: it proves the tests'
-own code, not the links (tools/gpu.sh multi_rehearse).  What only distinct
-GPUs have is skipped then: RCCL (it refuses two ranks on one GPU), the
-link table, and the "every pair spans two GPUs" check.
+On a box with ONE GPU visible (the driver's `pytest -m gpu` box) this module
+runs as its one-GPU rehearsal instead of skipping: a fixture sets
+MPX_MULTI_REHEARSE=1 and MPX_LL_MAX=8192 (the cross-GPU LL threshold) for
+each test (monkeypatch, not the whole run's environment; subprocess workers
+inherit them), every rank on GPU 0 and N = MPX_MULTI_REHEARSE_N (default 4)
+ranks where a test uses the whole node.  It proves the tests' own code, not
+the links.  What only distinct GPUs have is skipped then, with the reason:
+RCCL (it refuses two ranks on one GPU), the link table, and the "every pair
+spans two GPUs" check.  With two or more GPUs visible the distinct-GPU form
+runs; MPX_MULTI_REHEARSE=1 in the environment forces the rehearsal there too
+(tools/gpu.sh multi_rehearse).
 """
 import glob
 import json
@@ -33,7 +38,7 @@ import pytest
 
 import mpx
 import oracle_py as O
-from pairs import REHEARSE, Pairs, cross_gpu_devs
+from pairs import Pairs, cross_gpu_devs, rehearsing
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -54,19 +59,33 @@ def ngpus() -> int:
 # so a one-GPU run says what it did not measure.
 CFG = {
     "cfg3": "BASELINE cfg3 (2 x MI355X, one pair over xGMI): per-pair unidir GB/s at 4 MiB, target >= 85 % of "
-            "the link (65.3 GB/s of one direction's 76.8; 130.6 of the 153.6 bidirectional), and the 8 B "
-            "half round trip, target < 3 us",
+            "the link (130.6 GB/s of the stated 153.6 per direction, SURVEY.md:361; 65.3 of 76.8 beside it, the "
+            "unsourced per-direction reading), and the 8 B half round trip, target < 3 us",
     "cfg4": "BASELINE cfg4 (8 x MI355X, all 28 pairs in concurrent rounds): every pair's payloads checked, "
             "aggregate GB/s per round reported (bench.py)",
     "cfg5": "BASELINE cfg5 (8 x MI355X, RCCL all-pairs stress): every payload checksummed, receive digests = "
             "the reference's, kusto_ingest-ready records",
 }
-XGMI_ONE_DIRECTION_GBPS, XGMI_BIDIR_GBPS = 76.8, 153.6
+# STATED: ~153 GB/s per link per direction as SURVEY.md:361 / BASELINE.md:51
+# state the bar (the primary verdict); READING: 153.6 read as both directions
+# summed, 76.8 each way (from memory, unsourced until a node run)
+XGMI_STATED_PER_DIRECTION_GBPS, XGMI_PER_DIRECTION_READING_GBPS = 153.6, 76.8
 TARGET_LINK_FRAC, TARGET_HALF_RTT_US = 0.85, 3.0
 
 
+@pytest.fixture(autouse=True)
+def one_gpu_rehearsal(monkeypatch):
+    """One GPU visible: this test runs in its rehearsal form (every rank on
+    GPU 0, the cross-GPU LL threshold), set for this test only."""
+    if rehearsing() or ngpus() == 1:
+        monkeypatch.setenv("MPX_MULTI_REHEARSE", "1")
+        monkeypatch.setenv("MPX_LL_MAX", "8192")
+        monkeypatch.setenv("MPX_MULTI_REHEARSE_N", os.environ.get("MPX_MULTI_REHEARSE_N", "4"))
+    yield
+
+
 def need(n: int, engine: str = "", distinct: bool = False, cfg: str = "cfg3"):
-    if REHEARSE:
+    if rehearsing():
         if engine == "rccl" or distinct:
             pytest.skip(f"needs distinct GPUs (one-GPU rehearsal); {CFG[cfg]}")
         assert os.environ.get("MPX_LL_MAX") == "8192", "rehearse with the cross-GPU LL threshold: MPX_LL_MAX=8192"
@@ -273,10 +292,10 @@ def test_cfg3_8B_half_rtt_reported_against_3us_target(record_property):
 def test_cfg3_unidir_4MiB_reported_against_85pct_link_target(record_property):
     """One pair, unidir 4 MiB x 500 (the bench's headline shape, G1 -> G0
     over one link): per-pair GB/s from the G1 launch's device time, reported
-    beside north_star's >= 85 % of link peak, against one direction of the
-    link (76.8 GB/s, the unidirectional loop's ceiling) and against the
-    153.6 GB/s bidirectional figure BASELINE.md quotes.  Fails only on a
-    broken measurement (< 1 GB/s)."""
+    beside north_star's >= 85 % of link peak.  The primary verdict is against
+    the stated bar (153.6 GB/s per link per direction, SURVEY.md:361); the
+    per-direction reading (76.8 GB/s each way, DESIGN.md §7, unsourced) is
+    reported beside it.  Fails only on a broken measurement (< 1 GB/s)."""
     need(2)
     n, iters = 4 << 20, 500
     P = Pairs("kernel", 1, n, fill="seeded", devs=cross_gpu_devs(2))
@@ -286,11 +305,7 @@ def test_cfg3_unidir_4MiB_reported_against_85pct_link_target(record_property):
         out, errs = P.run(mpx.MODE_UNIDIR, n, iters, check=False)
         assert not errs, errs
         gbps = n * iters / out[0].device_s / 1e9
-        report_target(record_property, "cfg3_unidir_4MiB_GBps", gbps, "GB/s",
-                      f">= {TARGET_LINK_FRAC} x {XGMI_ONE_DIRECTION_GBPS} (one direction)",
-                      gbps >= TARGET_LINK_FRAC * XGMI_ONE_DIRECTION_GBPS)
-        report_target(record_property, "cfg3_unidir_4MiB_frac_of_bidirectional_link", gbps / XGMI_BIDIR_GBPS, "",
-                      f">= {TARGET_LINK_FRAC} of {XGMI_BIDIR_GBPS} GB/s", gbps >= TARGET_LINK_FRAC * XGMI_BIDIR_GBPS)
+        report_link_targets(record_property, "cfg3_unidir_4MiB", gbps)
         assert gbps > 1
         # the same loop pulled (MPX_XFER_PULL: G0 loads G1's tx over the
         # link), every payload checked first; reported beside the push
@@ -299,12 +314,20 @@ def test_cfg3_unidir_4MiB_reported_against_85pct_link_target(record_property):
         out, errs = P.run(mpx.MODE_UNIDIR, n, iters, check=False, pull=True)
         assert not errs, errs
         pull_gbps = n * iters / out[0].device_s / 1e9
-        report_target(record_property, "cfg3_pull_unidir_4MiB_GBps", pull_gbps, "GB/s",
-                      f">= {TARGET_LINK_FRAC} x {XGMI_ONE_DIRECTION_GBPS} (one direction)",
-                      pull_gbps >= TARGET_LINK_FRAC * XGMI_ONE_DIRECTION_GBPS)
+        report_link_targets(record_property, "cfg3_pull_unidir_4MiB", pull_gbps)
         assert pull_gbps > 1
     finally:
         P.close()
+
+
+def report_link_targets(record_property, name: str, gbps: float) -> None:
+    """The primary verdict against the stated bar, the reading beside it."""
+    report_target(record_property, f"{name}_GBps", gbps, "GB/s",
+                  f">= {TARGET_LINK_FRAC} x {XGMI_STATED_PER_DIRECTION_GBPS} per direction (SURVEY.md:361)",
+                  gbps >= TARGET_LINK_FRAC * XGMI_STATED_PER_DIRECTION_GBPS)
+    report_target(record_property, f"{name}_GBps_per_direction_reading", gbps, "GB/s",
+                  f">= {TARGET_LINK_FRAC} x {XGMI_PER_DIRECTION_READING_GBPS} (unsourced per-direction reading, "
+                  f"DESIGN.md §7)", gbps >= TARGET_LINK_FRAC * XGMI_PER_DIRECTION_READING_GBPS)
 
 
 # ---- mpx_perf on every GPU of the node -------------------------------------
@@ -326,7 +349,7 @@ def _files(tmp_path):
 
 
 def _world():
-    if REHEARSE:
+    if rehearsing():
         return int(os.environ.get("MPX_MULTI_REHEARSE_N", "4"))
     n = ngpus()
     return n - (n & 1)
@@ -351,7 +374,7 @@ def test_cfg4_all_pairs_rounds_every_gpu(tmp_path, engine):
     assert {(int(f[2]), int(f[6])) for f in side} == {q for rnd in all_pairs_rounds(N) for q in rnd}
     assert len(recs) == (N - 1) * (N // 2)
     assert all(int(f[16]) == 0 and int(f[15]) == 10 and int(f[18]) == 10 for f in side)
-    if not REHEARSE:
+    if not rehearsing():
         assert all(f[5] != f[7] for f in side)             # every pair spans two GPUs
 
 

@@ -46,3 +46,33 @@ def test_rank_streams_destroyed_and_recreated_every_cycle(engine, npairs):
     r = subprocess.run([sys.executable, "-u", "-c", code], capture_output=True, text=True, timeout=100,
                        env=dict(os.environ))
     assert r.returncode == 0 and "cycles done 30" in r.stdout, (r.returncode, r.stdout[-400:], r.stderr[-800:])
+
+
+@pytest.mark.parametrize("nbytes,iters", [(1 << 20, 4), (64 << 20, 2), (4096, 1)])
+def test_failed_copy_leaks_no_event_and_the_next_copy_works(monkeypatch, nbytes, iters):
+    """MPX_TEST=fail_copy: mpx_copy fails after both of its events were
+    created and the start one recorded (an early return through HIPCK's
+    path).  The events are owned by RAII holders: the
+    process's live-event count is the same after the failure, and a normal
+    copy in the same context then succeeds and copies (every copy form:
+    pipe, a launch per copy, one launch)."""
+    import mpx
+    c = mpx.Context(1, "kernel")
+    try:
+        src, dst = c.alloc(0, nbytes), c.alloc(0, nbytes)
+        c.fill(src, nbytes, mpx.FILL_SPLITMIX, mpx.pattern_key(mpx.PATTERN_SEED, 5, 0, 0))
+        c.fill(dst, nbytes, mpx.FILL_BYTE, 0)
+        before = mpx.live_events()
+        for _ in range(3):
+            monkeypatch.setenv("MPX_TEST", "fail_copy")
+            with pytest.raises(mpx.MpxError, match="fail_copy"):
+                c.copy(0, dst, src, nbytes, iters)
+            monkeypatch.setenv("MPX_TEST", "")
+            assert mpx.live_events() == before
+        t = c.copy(0, dst, src, nbytes, iters)
+        assert t.launches >= 1 and mpx.live_events() == before
+        assert c.checksum(dst, nbytes) == c.checksum(src, nbytes)
+    finally:
+        monkeypatch.setenv("MPX_TEST", "")
+        c.close()
+    assert mpx.live_events() == before   # the context attached no rank: it held no event of its own

@@ -18,12 +18,25 @@ the bench uses, and both counter views are read per case:
                 host_noncoherent hipHostMalloc(hipHostMallocNonCoherent)
                 ipc_import       this GPU's hipMalloc, opened with hipIpcOpenMemHandle in a
                                  second process that writes it (copy writer)
+                peer_hbm_ipc     GPU 1's HBM (an mpx_alloc on GPU 1), opened with
+                                 hipIpcOpenMemHandle in a second process on GPU 0 that
+                                 writes it (copy writer): bench.py's one-process-per-GPU
+                                 path, known bytes across xGMI
+                peer_hbm         bench.peer_link_control, the identical in-process case
+                                 bench.py runs on the node (k_copy, then k_xfer unidir,
+                                 GPU 0 -> GPU 1 with peer access)
   passes        A  TCC_EA0_WRREQ_sum, TCC_EA0_WRREQ_64B_sum, TCC_EA0_WRREQ_DRAM_sum
                 B  TCC_EA0_WRREQ_WRITE_GMI_32B_sum, _WRITE_IO_32B_sum, _WRITE_DRAM_32B_sum
 
 Per case: subtraction_over_algorithmic = (WRREQ - WRREQ_DRAM) x 64 / bytes,
-gmi / io / dram_over_algorithmic = the 32-B counters x 32 / bytes.  Prints
-one JSON document (profiles/r05_link_counter_control.json).
+gmi / io / dram_over_algorithmic = the 32-B counters x 32 / bytes.  For the
+two peer-HBM cases `peer_table` reports every EA write counter (WRREQ,
+WRREQ_DRAM, WRREQ_WRITE_GMI_32B, WRREQ_WRITE_IO_32B) as a multiple of the
+known bytes, and `peer_formula` picks the link-byte formula from that table:
+the first of bench.LINK_FORMULAS that reads the bytes within
+bench.PEER_CONTROL_BAND in every peer case whose copy checked (None, with the
+reason, on one GPU or when none does).  Prints one JSON document
+(profiles/r05_link_counter_control.json; round 6 adds the peer cases).
 
     python3 tools/link_counter_control.py
     python3 tools/link_counter_control.py child <handle-hex> <bytes> <iters>   (internal)
@@ -110,6 +123,79 @@ def summarise(vals, nbytes):
                                                        else None))
 
 
+def peer_table(cases: dict, nbytes: int) -> dict:
+    """every EA write counter of each peer case as a multiple of the known
+    bytes (raw counter x its unit / bytes), and the formulas' readings"""
+    units = {"TCC_EA0_WRREQ_sum": 64, "TCC_EA0_WRREQ_DRAM_sum": 64, "TCC_EA0_WRREQ_WRITE_GMI_32B_sum": 32,
+             "TCC_EA0_WRREQ_WRITE_IO_32B_sum": 32}
+    out = {}
+    for name, vals in cases.items():
+        row = {k: (round(vals[k] * u / nbytes, 5) if k in vals else None) for k, u in units.items()}
+        row["formulas"] = {k: round(v / nbytes, 5) for k, v in bench_formulas(vals).items()}
+        row["checked"] = vals.get("checked")
+        out[name] = row
+    return out
+
+
+def bench_formulas(vals: dict) -> dict:
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.link_formula_bytes(vals)
+
+
+def peer_formula(table: dict, distinct: bool) -> dict:
+    """the formula the table supports: the first of bench.LINK_FORMULAS whose
+    reading lies in bench.PEER_CONTROL_BAND in every peer case that checked
+    its copy"""
+    sys.path.insert(0, ROOT)
+    import bench
+    lo, hi = bench.PEER_CONTROL_BAND
+    if not distinct:
+        return dict(formula=None, reason="one GPU: no peer HBM, nothing to validate (the code path only)")
+    rows = {k: v for k, v in table.items() if v.get("checked")}
+    if not rows:
+        return dict(formula=None, reason="no peer case checked its copy")
+    for f in bench.LINK_FORMULAS:
+        got = [r["formulas"].get(f) for r in rows.values()]
+        if all(x is not None and lo <= x <= hi for x in got):
+            return dict(formula=f, band=[lo, hi], readings={k: r["formulas"][f] for k, r in rows.items()})
+    return dict(formula=None, band=[lo, hi], reason="no formula reads the known bytes in every peer case")
+
+
+def peer_cases(mpx, counters, H, c, src, bus, peer, run_child) -> dict:
+    """The peer-HBM cases: GPU 0 writes B x ITERS known bytes into GPU
+    `peer`'s HBM, (1) from a second process that IPC-imported an mpx_alloc
+    of GPU `peer` (run_child(handle_hex) -> its case JSON), (2) by
+    bench.peer_link_control in this process (the identical case bench.py
+    runs on the node).  Returns the cases, the table and the formula."""
+    sys.path.insert(0, ROOT)
+    import bench
+    out = {}
+    vals = {}
+    dst = c.alloc(peer, B)
+    try:
+        h = IpcHandle()
+        ck(H.hipIpcGetMemHandle(C.byref(h), C.c_void_p(dst.ptr)), "hipIpcGetMemHandle (peer)")
+        case = run_child(C.string_at(C.addressof(h), 64).hex())
+        if isinstance(case, dict):
+            case["copy_checked_by_owner"] = c.checksum(dst, B) == c.checksum(src, B)
+            vals["peer_hbm_ipc"] = dict(case["counters"], checked=bool(case.get("copy_checked")
+                                                                        and case["copy_checked_by_owner"]))
+        out["copy->peer_hbm_ipc"] = case
+    finally:
+        c.free(dst)
+    try:
+        pc = bench.peer_link_control(mpx, counters, bus, 0, peer)
+        out["peer_link_control"] = dict(pc, note="GPU 0 -> GPU %d across xGMI" % peer if peer else
+                                        "one GPU: GPU 0 -> GPU 0 (local DRAM), the code path only")
+        if isinstance(pc.get("copy"), dict) and "raw" in pc["copy"]:
+            vals["peer_hbm"] = dict(pc["copy"]["raw"], checked=bool(pc.get("copy_checked")))
+    except Exception as e:  # noqa: BLE001
+        out["peer_link_control"] = f"{type(e).__name__}: {e}"[:300]
+    table = peer_table(vals, B * ITERS)
+    return dict(cases=out, peer_table=table, peer_formula=peer_formula(table, peer != 0))
+
+
 def child(handle_hex, nbytes, iters):
     counters.register()
     import mpx
@@ -164,6 +250,15 @@ def main():
         ck(H.hipMalloc(C.byref(p), B), "hipMalloc")
         return p.value, lambda: H.hipFree(p)
 
+    def run_child(handle_hex):
+        r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "child", handle_hex, str(B), str(ITERS)],
+                           capture_output=True, text=True, timeout=150)
+        try:
+            return json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception:  # noqa: BLE001
+            return f"child rc {r.returncode}: {r.stderr[-400:]}"
+
+    peer = 1 if mpx.device_count() > 1 else 0
     with mpx.Context(2, "kernel") as c:
         src, src1, rx0 = c.alloc(0, B), c.alloc(0, B), c.alloc(0, B)
         c.fill(src, B, mpx.FILL_SPLITMIX, 1)
@@ -221,29 +316,19 @@ def main():
         ipc = c.alloc(0, B)
         h = IpcHandle()
         ck(H.hipIpcGetMemHandle(C.byref(h), C.c_void_p(ipc.ptr)), "hipIpcGetMemHandle")
-        r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "child",
-                            C.string_at(C.addressof(h), 64).hex(), str(B), str(ITERS)],
-                           capture_output=True, text=True, timeout=150)
-        try:
-            out["cases"]["copy->ipc_import"] = json.loads(r.stdout.strip().splitlines()[-1])
-            out["cases"]["copy->ipc_import"]["copy_checked_by_owner"] = c.checksum(ipc, B) == c.checksum(src, B)
-        except Exception:  # noqa: BLE001
-            out["cases"]["copy->ipc_import"] = f"child rc {r.returncode}: {r.stderr[-400:]}"
-        for b in (ipc,):
-            c.free(b)
-    # bench.py's on-node control (bench.peer_link_control): known bytes from
-    # GPU 0 into another GPU's HBM when there is one — the destination one
-    # GPU cannot show — else GPU 0 into itself (local DRAM: exercises the
-    # same code, validates nothing)
-    sys.path.insert(0, ROOT)
-    import bench
-    peer = 1 if mpx.device_count() > 1 else 0
-    try:
-        out["peer_link_control"] = dict(bench.peer_link_control(mpx, counters, bus, 0, peer),
-                                        note="GPU 0 -> GPU 1 across xGMI" if peer else
-                                        "one GPU: GPU 0 -> GPU 0 (local DRAM), the code path only")
-    except Exception as e:  # noqa: BLE001
-        out["peer_link_control"] = f"{type(e).__name__}: {e}"[:300]
+        case = run_child(C.string_at(C.addressof(h), 64).hex())
+        if isinstance(case, dict):
+            case["copy_checked_by_owner"] = c.checksum(ipc, B) == c.checksum(src, B)
+        out["cases"]["copy->ipc_import"] = case
+        c.free(ipc)
+        # the peer-HBM cases: known bytes from GPU 0 into another GPU's HBM
+        # when there is one — the destination one GPU cannot show — else GPU
+        # 0 into itself (local DRAM: exercises the same code, validates
+        # nothing); the table of every EA write counter and the formula
+        pc = peer_cases(mpx, counters, H, c, src, bus, peer, run_child)
+        out["cases"].update(pc["cases"])
+        out["peer_link_control"] = out["cases"].pop("peer_link_control")
+        out["peer_table"], out["peer_formula"] = pc["peer_table"], pc["peer_formula"]
     mpx.shutdown()
     print(json.dumps(out, indent=1))
     return 0

@@ -21,6 +21,9 @@
 #       rank 0 is counter-profiled (the GPU's counters are shared), and every
 #       write lands in local DRAM, so the link traffic reads 0
 # Each rank has its own time limit; the script fails if any rank fails.
+# --no-cpu-baseline on every rank: a profiled rank must start no mpiexec chain
+# (the profiler's preload would reach oracle/ref_wrap.sh's exec after the GPU
+# was initialised; bench.py also refuses the reference legs under a profiler).
 set -o pipefail
 N=${N:-2}
 O=gpurun_out/node_prof_n$N
@@ -39,10 +42,11 @@ run_pass() {   # pass-name, rocprofv3 options...
         if [ -n "$MPX_BENCH_ONE_GPU" ] && [ "${pass%trace}" = "$pass" ] && [ $r -gt 0 ]; then prof=(); fi
         if [ ${#prof[@]} -gt 0 ]; then
             RANK=$r LOCAL_RANK=$r timeout -k 10 300 rocprofv3 "${prof[@]}" --output-format csv -d $O/$pass -o rank$r \
-                -- python3 -u bench.py --gpus $N --steps $STEPS --warmup 1 --no-extras \
+                -- python3 -u bench.py --gpus $N --steps $STEPS --warmup 1 --no-extras --no-cpu-baseline \
                 > $O/${pass}_rank$r.json 2> $O/${pass}_rank$r.err &
         else
             RANK=$r LOCAL_RANK=$r timeout -k 10 300 python3 -u bench.py --gpus $N --steps $STEPS --warmup 1 --no-extras \
+                --no-cpu-baseline \
                 > $O/${pass}_rank$r.json 2> $O/${pass}_rank$r.err &
         fi
         pids+=($!)
