@@ -191,7 +191,7 @@ def descendants(root: int | None = None) -> list[dict]:
     return out
 
 
-def run_reference(nranks: int, ppn: int, args: list[str], timeout: float) -> dict:
+def run_reference(nranks: int, ppn: int, args: list[str], timeout: float, placement: list[str] | None = None) -> dict:
     """One mpiexec run of the compiled reference (oracle/_ref) under MPICH
     shared memory, its ranks bound like its launchers bind them
     (reference_cores: `-bind-to user:<cores>`, `-membind bind:<node>`).
@@ -199,7 +199,9 @@ def run_reference(nranks: int, ppn: int, args: list[str], timeout: float) -> dic
     still alive when it returns (or times out) is named in `leftover` and
     killed, so no hydra proxy or rank outlives the leg (VERDICT r05, next 3;
     the reference itself finalizes cleanly, mpi_perf.c:579-581).  Returns
-    rc, stderr tail, the records' (run, time_s) pairs, binding, leftover."""
+    rc, stderr tail, the records' (run, time_s) pairs, binding, leftover.
+    `placement` (tools/ref_placement.py) replaces the binding arguments:
+    one form, tried once ([] = mpiexec's default placement)."""
     import signal
     pick = reference_cores(nranks)
     tmp = tempfile.mkdtemp(prefix="cpu_base_")
@@ -216,6 +218,8 @@ def run_reference(nranks: int, ppn: int, args: list[str], timeout: float) -> dic
             + ["-l", "logs"]
         forms = [["-bind-to", "user:" + ",".join(map(str, pick["cores"])), "-membind", f"bind:{pick['numa_node']}"],
                  ["-bind-to", "user:" + ",".join(map(str, pick["cores"]))], []] if pick["complete"] else [[]]
+        if placement is not None:
+            forms = [placement]
         for form in forms:
             for x in glob.glob(os.path.join(tmp, "logs", "*")):
                 os.remove(x)
@@ -246,7 +250,9 @@ def run_reference(nranks: int, ppn: int, args: list[str], timeout: float) -> dic
                 out["times"].append((int(f[10]), float(f[9]) / 1000.0))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    if not out["cores"] or out["binding"].startswith("none"):
+    if placement is not None:
+        out["cores"] = None   # the caller's placement, named by `binding`
+    elif not out["cores"] or out["binding"].startswith("none"):
         out["cores"] = None
     return out
 

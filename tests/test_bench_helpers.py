@@ -125,3 +125,12 @@ def test_reference_legs_not_started_under_a_profiler(monkeypatch):
     src = open(bench.__file__).read()
     main = src[src.index("def main()"):]
     assert main.index("prof_var = under_profiler()") < main.index("cpu_baseline(nbytes")
+
+
+def test_run_reference_with_an_explicit_placement():
+    """tools/ref_placement.py's A/B: run_reference with a caller's placement
+    runs that one form (here mpiexec's default), names it, and leaves no
+    process behind."""
+    r = bench.run_reference(2, 1, ["-u", "1", "-b", "65536", "-i", "50", "-r", "3"], 60, placement=[])
+    assert r["rc"] == 0 and r["binding"].startswith("none") and r["cores"] is None, r
+    assert len(r["times"]) == 2 and r["leftover"] == [] and bench.descendants() == []

@@ -155,7 +155,7 @@ def test_link_counter_control_peer_cases_pick_the_formula(peer, per_byte, want):
     def run_child(handle_hex):
         seen.append(handle_hex)
         vals = {n: per_byte.get(n, 0.0) * nbytes / u for n, u in unit.items()}
-        return dict(T.summarise(dict(vals, TCC_EA0_WRREQ_64B_sum=0.0), nbytes), copy_checked=True)
+        return dict(T.summarise(dict(vals, TCC_EA0_WRREQ_64B_sum=0.0), nbytes), copy_checked=True, src_checksum=7)
 
     c = _Ctx()
     r = T.peer_cases(_Mpx, counters, _Hip, c, c.alloc(0, 16), "bus0", peer, run_child)

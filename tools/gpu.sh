@@ -16,6 +16,7 @@
 #   stall            tools/exit_stall_repro: fenced vs barrier stream teardown cycles
 #   procs_exit       mpx_perf processes mode (2 processes on GPU 0), exit with mpx_shutdown, K runs
 #   linkctl          tools/link_counter_control.py: the link-byte counter's positive control
+#   refplace         tools/ref_placement.py: the reference's host rate under each rank placement (CPU only)
 #   soak             tools/soak.py: threads + processes + SDMA, then the two negative controls
 #   fuzz             the live-reference parity fuzz tests (MPX_FUZZ_EXAMPLES, default 150)
 #   multi_rehearse   tests/test_gpu_multi.py with every rank on GPU 0 (MPX_MULTI_REHEARSE)
@@ -210,6 +211,9 @@ for s in "$@"; do
     linkctl)
         timeout -k 10 200 python3 -u tools/link_counter_control.py > $O/link_counter_control.json 2> $O/link_counter_control.err
         step_ok linkctl $? ;;
+    refplace)
+        timeout -k 10 600 python3 -u tools/ref_placement.py 3 > $O/ref_placement.json 2> $O/ref_placement.err
+        step_ok refplace $? ;;
     soak)
         soak; step_ok soak $? ;;
     fuzz)
