@@ -157,57 +157,103 @@ def reference_cores(nranks: int, sysfs: str = "/sys/devices/system") -> dict:
                 complete=len(chosen) == nranks)
 
 
-def _proc_group(pgid: int) -> list[dict]:
-    """The processes of process group pgid (from /proc): pid, ppid, name."""
-    out = []
-    for d in glob.glob("/proc/[0-9]*"):
-        st = _read(os.path.join(d, "stat"))
-        if not st:
-            continue
-        name = st[st.index("(") + 1:st.rindex(")")]
-        f = st[st.rindex(")") + 2:].split()
-        if int(f[2]) == pgid:
-            out.append(dict(pid=int(os.path.basename(d)), ppid=int(f[1]), name=name))
-    return out
-
-
-def descendants(root: int | None = None) -> list[dict]:
-    """Every live process below `root` (default: this one) in the parent
-    tree, from /proc: pid, ppid, name, state (bench.py's exit census)."""
-    root = os.getpid() if root is None else root
+def _procs() -> dict:
+    """Every live process from /proc: pid -> pid, ppid, name, state, start
+    (the start time in clock ticks after boot: with the pid it names one
+    process, whatever pids are reused later)."""
     procs = {}
     for d in glob.glob("/proc/[0-9]*"):
         st = _read(os.path.join(d, "stat"))
-        if not st:
+        if not st or ")" not in st:
             continue
         f = st[st.rindex(")") + 2:].split()
-        procs[int(os.path.basename(d))] = dict(pid=int(os.path.basename(d)), ppid=int(f[1]), state=f[0],
-                                               name=st[st.index("(") + 1:st.rindex(")")])
+        pid = int(os.path.basename(d))
+        procs[pid] = dict(pid=pid, ppid=int(f[1]), state=f[0], start=int(f[19]),
+                          name=st[st.index("(") + 1:st.rindex(")")])
+    return procs
+
+
+def descendants(root: int | None = None, procs: dict | None = None) -> list[dict]:
+    """Every live process below `root` (default: this one) in the parent
+    tree, from /proc: pid, ppid, name, state, start (bench.py's exit census;
+    zombies not yet reaped by their parent are listed too)."""
+    root = os.getpid() if root is None else root
+    procs = _procs() if procs is None else procs
     out, frontier = [], {root}
     while frontier:
-        kids = [p for p in procs.values() if p["ppid"] in frontier and p["pid"] != root]
+        kids = [q for q in procs.values() if q["ppid"] in frontier and q["pid"] != root]
         out += kids
-        frontier = {p["pid"] for p in kids}
+        frontier = {q["pid"] for q in kids}
     return out
+
+
+def run_tracked(cmd: list[str], timeout: float, **popen_kw) -> dict:
+    """Run cmd to its end (or `timeout`), tracking every process below it.
+    MPICH's hydra puts each proxy and each rank in a session of its own
+    (setsid), so neither a process group nor a session can find them once
+    mpiexec is gone: their pids (with start times) are collected from the
+    parent tree while it runs, every 0.25 s.  When cmd returns, any of them
+    still alive (same pid and start time, not a zombie) is named in
+    `leftover` and killed.  stdout / stderr go to
+    files, so no descendant can hold a pipe open."""
+    import signal
+    seen = {}
+    with tempfile.TemporaryFile("w+") as fo, tempfile.TemporaryFile("w+") as fe:
+        p = subprocess.Popen(cmd, stdout=fo, stderr=fe, text=True, start_new_session=True, **popen_kw)
+        deadline, timed_out = time.monotonic() + timeout, False
+        while p.poll() is None:
+            for q in descendants(p.pid):
+                seen[q["pid"]] = q
+            if time.monotonic() > deadline:
+                timed_out = True
+                break
+            time.sleep(0.25)
+        if timed_out:
+            for q in descendants(p.pid):
+                seen[q["pid"]] = q
+            for sig_target in [p.pid] + list(seen):
+                try:
+                    os.kill(sig_target, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+        p.wait()
+        now = _procs()
+        left = [dict(pid=q["pid"], name=q["name"]) for q in seen.values()
+                if q["pid"] in now and now[q["pid"]]["start"] == q["start"] and now[q["pid"]]["state"] != "Z"]
+        for q in left:
+            try:
+                os.kill(q["pid"], signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+        if left:
+            print(f"[bench] {os.path.basename(cmd[0])} left {left} alive: killed", file=sys.stderr)
+        fo.seek(0)
+        fe.seek(0)
+        out, err = fo.read(), fe.read()
+    if timed_out:
+        err = f"timed out after {timeout} s; " + err
+    return dict(rc=p.returncode, stdout=out, stderr=err, leftover=left, tracked=len(seen), timed_out=timed_out)
 
 
 def run_reference(nranks: int, ppn: int, args: list[str], timeout: float, placement: list[str] | None = None) -> dict:
     """One mpiexec run of the compiled reference (oracle/_ref) under MPICH
     shared memory, its ranks bound like its launchers bind them
     (reference_cores: `-bind-to user:<cores>`, `-membind bind:<node>`).
-    mpiexec starts in a session of its own; whatever of its process group is
-    still alive when it returns (or times out) is named in `leftover` and
-    killed, so no hydra proxy or rank outlives the leg (VERDICT r05, next 3;
-    the reference itself finalizes cleanly, mpi_perf.c:579-581).  Returns
-    rc, stderr tail, the records' (run, time_s) pairs, binding, leftover.
+    Every process below mpiexec is tracked (run_tracked): none outlives the
+    leg (the reference itself finalizes cleanly, mpi_perf.c:579-581).  This
+    process keeps off the ranks' cores meanwhile (its own affinity without
+    them), so its polling never preempts a rank.  Returns rc, stderr tail,
+    the records' (run, time_s) pairs, binding, leftover.
     `placement` (tools/ref_placement.py) replaces the binding arguments:
     one form, tried once ([] = mpiexec's default placement)."""
-    import signal
     pick = reference_cores(nranks)
     tmp = tempfile.mkdtemp(prefix="cpu_base_")
     out = dict(rc=None, stderr="", times=[], leftover=[], binding=None, cores=pick["cores"],
-               numa_node=pick["numa_node"])
+               numa_node=pick["numa_node"], tracked=0)
+    mask = os.sched_getaffinity(0)
     try:
+        if pick["complete"] and mask - set(pick["cores"]):
+            os.sched_setaffinity(0, mask - set(pick["cores"]))
         with open(os.path.join(tmp, "group1"), "w") as f:
             f.write("localhost\n")
         os.mkdir(os.path.join(tmp, "logs"))
@@ -223,32 +269,19 @@ def run_reference(nranks: int, ppn: int, args: list[str], timeout: float, placem
         for form in forms:
             for x in glob.glob(os.path.join(tmp, "logs", "*")):
                 os.remove(x)
-            p = subprocess.Popen([MPIEXEC, "-np", str(nranks)] + form + tail, cwd=tmp, env=env,
-                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
-            try:
-                _, err = p.communicate(timeout=timeout)
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
-                _, err = p.communicate()
-                err = f"timed out after {timeout} s; " + (err or "")
-            finally:
-                left = [q for q in _proc_group(p.pid) if q["pid"] != p.pid]
-                if left:
-                    out["leftover"] += left
-                    print(f"[bench] reference leg left {left} alive: killed", file=sys.stderr)
-                try:
-                    os.killpg(p.pid, signal.SIGKILL)
-                except ProcessLookupError:
-                    pass
-            out["rc"], out["stderr"] = p.returncode, (err or "")[-400:]
+            r = run_tracked([MPIEXEC, "-np", str(nranks)] + form + tail, timeout, cwd=tmp, env=env)
+            out["leftover"] += r["leftover"]
+            out["tracked"] = max(out["tracked"], r["tracked"])
+            out["rc"], out["stderr"] = r["rc"], r["stderr"][-400:]
             out["binding"] = " ".join(form) if form else "none (mpiexec's default placement)"
-            if p.returncode == 0:
+            if r["rc"] == 0:
                 break
         for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log")):
             for line in open(path):
                 f = line.strip().split(",")
                 out["times"].append((int(f[10]), float(f[9]) / 1000.0))
     finally:
+        os.sched_setaffinity(0, mask)
         shutil.rmtree(tmp, ignore_errors=True)
     if placement is not None:
         out["cores"] = None   # the caller's placement, named by `binding`
@@ -263,7 +296,8 @@ def _spread(rates: list[float]) -> dict:
 
 
 def _placement(r: dict) -> dict:
-    return dict(core_list=r["cores"], numa_node=r["numa_node"], binding=r["binding"], leftover_processes=r["leftover"])
+    return dict(core_list=r["cores"], numa_node=r["numa_node"], binding=r["binding"], leftover_processes=r["leftover"],
+                processes_tracked=r["tracked"])
 
 
 def cpu_baseline(nbytes: int, iters: int, runs: int) -> dict | None:

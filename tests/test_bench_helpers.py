@@ -134,3 +134,23 @@ def test_run_reference_with_an_explicit_placement():
     r = bench.run_reference(2, 1, ["-u", "1", "-b", "65536", "-i", "50", "-r", "3"], 60, placement=[])
     assert r["rc"] == 0 and r["binding"].startswith("none") and r["cores"] is None, r
     assert len(r["times"]) == 2 and r["leftover"] == [] and bench.descendants() == []
+
+
+def test_run_tracked_names_and_kills_an_orphan_in_its_own_session():
+    """hydra puts every proxy and rank in a session of its own (setsid), so
+    bench.run_tracked follows the parent tree while the command runs: a
+    process that outlives the command in a new session is named and
+    killed."""
+    r = bench.run_tracked(["bash", "-c", "setsid sleep 30 & sleep 0.6; exit 0"], 20)
+    assert r["rc"] == 0 and not r["timed_out"] and r["tracked"] >= 1
+    assert [q["name"] for q in r["leftover"]] == ["sleep"], r
+    import time
+    time.sleep(0.2)
+    procs = bench._procs()
+    pid = r["leftover"][0]["pid"]
+    assert pid not in procs or procs[pid]["state"] == "Z" or procs[pid]["name"] != "sleep"
+
+
+def test_run_tracked_time_limit_kills_the_tree():
+    r = bench.run_tracked(["bash", "-c", "sleep 30 & sleep 30"], 0.6)
+    assert r["timed_out"] and r["rc"] != 0 and "timed out" in r["stderr"] and r["leftover"] == [], r
