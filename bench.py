@@ -208,23 +208,26 @@ def run_tracked(cmd: list[str], timeout: float, **popen_kw) -> dict:
                 timed_out = True
                 break
             time.sleep(0.25)
+        def alive(now):
+            # the same process (pid and start time: a reused pid is not it), not a zombie
+            return [q for q in seen.values()
+                    if q["pid"] in now and now[q["pid"]]["start"] == q["start"] and now[q["pid"]]["state"] != "Z"]
+
+        def kill(qs):
+            for q in qs:
+                try:
+                    os.kill(q["pid"], signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+
         if timed_out:
             for q in descendants(p.pid):
                 seen[q["pid"]] = q
-            for sig_target in [p.pid] + list(seen):
-                try:
-                    os.kill(sig_target, signal.SIGKILL)
-                except (ProcessLookupError, PermissionError):
-                    pass
+            p.kill()
+            kill(alive(_procs()))
         p.wait()
-        now = _procs()
-        left = [dict(pid=q["pid"], name=q["name"]) for q in seen.values()
-                if q["pid"] in now and now[q["pid"]]["start"] == q["start"] and now[q["pid"]]["state"] != "Z"]
-        for q in left:
-            try:
-                os.kill(q["pid"], signal.SIGKILL)
-            except (ProcessLookupError, PermissionError):
-                pass
+        left = [dict(pid=q["pid"], name=q["name"]) for q in alive(_procs())]
+        kill(left)
         if left:
             print(f"[bench] {os.path.basename(cmd[0])} left {left} alive: killed", file=sys.stderr)
         fo.seek(0)
