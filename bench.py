@@ -89,6 +89,8 @@ EXTRAS_DEADLINE_S = 150      # 64 MiB rounds + comparison engines at N > 1 (see 
 CEILING_BYTES, CEILING_ITERS = 64 << 20, 20   # extras: the kernel engine at 64 MiB (see main)
 
 
+# N = 1 baseline: 1 GiB x 40 per run (bound ranks move ~24 GB/s: ~1.7 s a run)
+CPU_BASELINE_ITERS = 40
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
 REF_SHIM = os.path.join(ROOT, "oracle", "_ref", "libshim.so")
 MPIEXEC = "/opt/conda/bin/mpiexec"
@@ -1631,7 +1633,8 @@ def main() -> None:
         # CU-masked rank stream keeps its own) fits.  Set before HIP starts.
         os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
     # CPU baseline first, before this process touches the GPU: N = 1, two
-    # ranks at 1 GiB (~2.2 s per run on the box: ~13 s of CPU work); N >= 2,
+    # bound ranks at 1 GiB x 40 (~1.7 s per run on the box, 6 runs: ~10 s,
+    # ~20 s of CPU work on the two cores); N >= 2,
     # the reference in run-hbv3's layout at the headline's B and iterations
     # (the other ranks wait in the process-group init meanwhile)
     cpu = None
@@ -1644,7 +1647,7 @@ def main() -> None:
         cpu = dict(value=None, unit="GB/s", cores=0, kind="reference",
                    sample=f"not run: this process runs under a profiler ({prof_var} set)")
     elif rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(nbytes, 16, 6) if one else cpu_baseline_pairs(world, nbytes, iters, 6)
+        cpu = cpu_baseline(nbytes, CPU_BASELINE_ITERS, 6) if one else cpu_baseline_pairs(world, nbytes, iters, 6)
         # BASELINE config 1 itself (the reference's 2-rank ping-pong at 8 B
         # and 4 MiB) beside every line, whatever the workload
         pp = cpu_baseline_pingpong()
