@@ -91,6 +91,11 @@ CEILING_BYTES, CEILING_ITERS = 64 << 20, 20   # extras: the kernel engine at 64 
 
 # N = 1 baseline: 1 GiB x 40 per run (bound ranks move ~24 GB/s: ~1.7 s a run)
 CPU_BASELINE_ITERS = 40
+# every reference leg of one bench run ends by this time.monotonic() (set in
+# main): at N >= 2 the other ranks wait in the process-group init meanwhile
+# (its 180 s timeout), so the legs together must end well inside it
+REF_BUDGET_S = 120.0
+_ref_deadline = [None]
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "mpi_perf")
 REF_SHIM = os.path.join(ROOT, "oracle", "_ref", "libshim.so")
 MPIEXEC = "/opt/conda/bin/mpiexec"
@@ -227,6 +232,9 @@ def run_tracked(cmd: list[str], timeout: float, **popen_kw) -> dict:
                 seen[q["pid"]] = q
             p.kill()
             kill(alive(_procs()))
+            t_end = time.monotonic() + 2.0     # SIGKILL lands asynchronously
+            while alive(_procs()) and time.monotonic() < t_end:
+                time.sleep(0.02)
         p.wait()
         left = [dict(pid=q["pid"], name=q["name"]) for q in alive(_procs())]
         kill(left)
@@ -274,12 +282,16 @@ def run_reference(nranks: int, ppn: int, args: list[str], timeout: float, placem
         for form in forms:
             for x in glob.glob(os.path.join(tmp, "logs", "*")):
                 os.remove(x)
-            r = run_tracked([MPIEXEC, "-np", str(nranks)] + form + tail, timeout, cwd=tmp, env=env)
+            left_s = timeout if _ref_deadline[0] is None else _ref_deadline[0] - time.monotonic()
+            if left_s < 2:
+                out["rc"], out["stderr"] = None, f"not run: the reference legs' {REF_BUDGET_S:.0f} s budget is spent"
+                break
+            r = run_tracked([MPIEXEC, "-np", str(nranks)] + form + tail, min(timeout, left_s), cwd=tmp, env=env)
             out["leftover"] += r["leftover"]
             out["tracked"] = max(out["tracked"], r["tracked"])
             out["rc"], out["stderr"] = r["rc"], r["stderr"][-400:]
             out["binding"] = " ".join(form) if form else "none (mpiexec's default placement)"
-            if r["rc"] == 0:
+            if r["rc"] == 0 or r["timed_out"]:   # a run that hung is not retried in another form
                 break
         for path in glob.glob(os.path.join(tmp, "logs", "tcp-*.log")):
             for line in open(path):
@@ -290,7 +302,7 @@ def run_reference(nranks: int, ppn: int, args: list[str], timeout: float, placem
         shutil.rmtree(tmp, ignore_errors=True)
     if placement is not None:
         out["cores"] = None   # the caller's placement, named by `binding`
-    elif not out["cores"] or out["binding"].startswith("none"):
+    elif not out["cores"] or not out["binding"] or out["binding"].startswith("none"):
         out["cores"] = None
     return out
 
@@ -1647,6 +1659,7 @@ def main() -> None:
         cpu = dict(value=None, unit="GB/s", cores=0, kind="reference",
                    sample=f"not run: this process runs under a profiler ({prof_var} set)")
     elif rank == 0 and not args.no_cpu_baseline:
+        _ref_deadline[0] = time.monotonic() + REF_BUDGET_S
         cpu = cpu_baseline(nbytes, CPU_BASELINE_ITERS, 6) if one else cpu_baseline_pairs(world, nbytes, iters, 6)
         # BASELINE config 1 itself (the reference's 2-rank ping-pong at 8 B
         # and 4 MiB) beside every line, whatever the workload

@@ -154,3 +154,15 @@ def test_run_tracked_names_and_kills_an_orphan_in_its_own_session():
 def test_run_tracked_time_limit_kills_the_tree():
     r = bench.run_tracked(["bash", "-c", "sleep 30 & sleep 30"], 0.6)
     assert r["timed_out"] and r["rc"] != 0 and "timed out" in r["stderr"] and r["leftover"] == [], r
+
+
+def test_reference_legs_share_one_time_budget(monkeypatch):
+    """At N >= 2 the other ranks wait in the process-group init (180 s) while
+    rank 0 runs the reference legs: they share REF_BUDGET_S, and a leg that
+    finds the budget spent runs nothing and says so."""
+    import time
+    assert bench.REF_BUDGET_S < 180
+    monkeypatch.setattr(bench, "_ref_deadline", [time.monotonic()])
+    r = bench.run_reference(2, 1, ["-u", "1", "-b", "64", "-i", "5", "-r", "2"], 60)
+    assert r["rc"] is None and "budget is spent" in r["stderr"] and r["times"] == [], r
+    assert bench.cpu_baseline_pingpong()["GBps_4MiB"] is None
