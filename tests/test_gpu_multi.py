@@ -378,6 +378,18 @@ def test_cfg4_all_pairs_rounds_every_gpu(tmp_path, engine):
         assert all(f[5] != f[7] for f in side)             # every pair spans two GPUs
 
 
+@pytest.mark.parametrize("engine", ["kernel", "sdma"])
+def test_cfg4_all_28_pairs_shape_rehearsed(tmp_path, monkeypatch, engine):
+    """The node's own shape in the one-GPU rehearsal: N = 8 ranks, 7 rounds
+    x 4 concurrent pairs = all 28 pairs (the rehearsal's default N is 4),
+    every payload checked; on a multi-GPU node the test above already runs
+    the whole node."""
+    if not rehearsing():
+        pytest.skip("multi-GPU node: test_cfg4_all_pairs_rounds_every_gpu runs the node's N")
+    monkeypatch.setenv("MPX_MULTI_REHEARSE_N", "8")
+    test_cfg4_all_pairs_rounds_every_gpu(tmp_path, engine)
+
+
 def test_cfg5_rccl_all_pairs_stress_processes(tmp_path):
     """BASELINE config 5: one mpx_perf process per GPU (the reference's
     process model), RCCL engine, all-pairs rounds twice over, seeded payloads
