@@ -29,6 +29,7 @@
 #                    GPUs): the link-counter control across GPU 0 -> 1, the
 #                    multi-GPU suite on distinct GPUs, bench.py at N = 2, 4, 8
 #                    (one rank per GPU), then tools/node_profile.sh at N = 8
+#   node_rehearse    the same recipe on one GPU (every rank on GPU 0)
 # Environment: K (procs_exit runs, default 8), STALL_CYCLES (default 2000),
 # STALL_RUNS (default 3).
 # Round 4's per-pass wrappers (gpu_r04*.sh) and the older single-purpose
@@ -243,20 +244,27 @@ for s in "$@"; do
             -d $O/prof_sdma -o sdma -- $PERF -w 2 -e sdma -f $O/group1 -n 1 -p 1 -u 1 -b 4194304 -i 200 -r 3 \
             -l $O/logs_sdma > $O/prof_sdma.log 2>&1
         step_ok prof_sdma $? ;;
-    node)
+    node|node_rehearse)
+        # node_rehearse: the same script on ONE GPU (every rank on GPU 0:
+        # MPX_BENCH_ONE_GPU for bench.py and node_profile.sh, the multi-GPU
+        # suite's own rehearsal), so the node run's recipe itself is proven
         ngpu=$(python3 -c 'import sys; sys.path.insert(0, "mpi-perf_amd"); import mpx; print(mpx.device_count())')
-        [ "$ngpu" -ge 8 ] || { echo "node: $ngpu GPU(s) visible, 8 needed"; exit 2; }
+        one=""
+        if [ $s = node_rehearse ]; then one=1; else
+            [ "$ngpu" -ge 8 ] || { echo "node: $ngpu GPU(s) visible, 8 needed"; exit 2; }
+        fi
         timeout -k 10 300 python3 -u tools/link_counter_control.py > $O/link_counter_control.json 2> $O/link_counter_control.err
         step_ok "node linkctl" $?
         timeout -k 10 1200 python3 -u -m pytest tests/test_gpu_multi.py -m gpu -x -v --timeout 300 --timeout-method thread \
             > $O/pytest_multi.log 2>&1
         step_ok "node multi-GPU suite" $?
         for n in 2 4 8; do
-            timeout -k 10 900 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-                --master-port $((29700 + n)) bench.py --gpus $n > $O/bench_node_n$n.json 2> $O/bench_node_n$n.err
+            MPX_BENCH_ONE_GPU=$one timeout -k 10 900 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+                --master-addr 127.0.0.1 --master-port $((29700 + n)) bench.py --gpus $n \
+                > $O/bench_node_n$n.json 2> $O/bench_node_n$n.err
             step_ok "node bench n$n" $?
         done
-        N=8 tools/node_profile.sh > $O/node_profile_n8.log 2>&1
+        N=8 MPX_BENCH_ONE_GPU=$one tools/node_profile.sh > $O/node_profile_n8.log 2>&1
         step_ok "node profile n8" $? ;;
     node_profile2)
         N=2 MPX_BENCH_ONE_GPU=1 tools/node_profile.sh > $O/node_profile_n2.log 2>&1

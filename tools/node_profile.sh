@@ -29,6 +29,10 @@ N=${N:-2}
 O=gpurun_out/node_prof_n$N
 mkdir -p $O
 export TMPDIR=/tmp WORLD_SIZE=$N MASTER_ADDR=127.0.0.1
+# one-GPU rehearsal: one HW queue per process, as bench.py sets for itself —
+# set here, before the process starts, because the profiler may start HIP
+# before bench.py's own line runs
+[ -n "$MPX_BENCH_ONE_GPU" ] && export GPU_MAX_HW_QUEUES=1
 # Under rocprofv3 bench.py destroys its rank streams (mpx_shutdown) and exits
 # normally, so the profiler's exit-time finalizer writes the output and finds
 # no live CU-masked queue (profiles/r04_exit_segv_stack.txt)
