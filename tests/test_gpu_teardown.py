@@ -76,3 +76,44 @@ def test_failed_copy_leaks_no_event_and_the_next_copy_works(monkeypatch, nbytes,
         monkeypatch.setenv("MPX_TEST", "")
         c.close()
     assert mpx.live_events() == before   # the context attached no rank: it held no event of its own
+
+
+SHUTDOWN_TWICE = """
+import sys
+sys.path.insert(0, {pkg!r}); sys.path.insert(0, {here!r})
+import mpx
+from pairs import Pairs
+P = Pairs("kernel", 1, 1 << 16, fill="seeded")
+try:
+    out, errs = P.run(mpx.MODE_UNIDIR, 4096, 3)
+    assert not errs and all(o.check_failures == 0 for o in out.values()), errs
+finally:
+    P.close()
+mpx.shutdown()
+mpx.shutdown()          # nothing pooled: a no-op, not a second destroy of the same streams
+P = Pairs("kernel", 1, 1 << 16, fill="seeded")   # fresh rank streams
+try:
+    out, errs = P.run(mpx.MODE_PINGPONG, 4096, 3)
+    assert not errs and all(o.check_failures == 0 for o in out.values()), errs
+    try:
+        mpx.shutdown()  # a context is alive: refused, nothing destroyed
+        raise SystemExit("shutdown with a live context was not refused")
+    except mpx.MpxError as e:
+        assert e.status == mpx.ERR_STATE, e
+    out, errs = P.run(mpx.MODE_PINGPONG, 4096, 3)
+    assert not errs, errs
+finally:
+    P.close()
+mpx.shutdown()
+print("shutdown ok", flush=True)
+"""
+
+
+def test_shutdown_twice_and_refused_while_a_context_lives():
+    """mpx_shutdown forgets every stream it destroyed: a second
+    call is a no-op; while a context is alive it is refused (MPX_ERR_STATE)
+    and the context's streams keep working; a later context gets fresh ones."""
+    code = SHUTDOWN_TWICE.format(pkg=os.path.join(os.path.dirname(HERE), "mpi-perf_amd"), here=HERE)
+    r = subprocess.run([sys.executable, "-u", "-c", code], capture_output=True, text=True, timeout=100,
+                       env=dict(os.environ))
+    assert r.returncode == 0 and "shutdown ok" in r.stdout, (r.returncode, r.stdout[-400:], r.stderr[-800:])
